@@ -1,0 +1,116 @@
+// Shared host/device definitions: the trial-stream randomness spec (Philox4x32-10)
+// and the convolutional-code description in the reference's convention.
+//
+// The randomness spec is the build's own (the reference never seeds its trial
+// simulations and its simulator is missing — SURVEY.md §0.1, §8 row A5); it is
+// restated independently in oracle/philox.py and oracle/cvd_oracle.c and the
+// three are checked against each other by the tests.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define CVD_HD __host__ __device__ __forceinline__
+#else
+#define CVD_HD inline
+#endif
+
+namespace cvd {
+
+constexpr uint32_t kPhiloxM0 = 0xD2511F53u;
+constexpr uint32_t kPhiloxM1 = 0xCD9E8D57u;
+constexpr uint32_t kPhiloxW0 = 0x9E3779B9u;
+constexpr uint32_t kPhiloxW1 = 0xBB67AE85u;
+constexpr uint32_t kKindNoise = 0;
+constexpr uint32_t kKindInput = 1;
+constexpr uint32_t kLearnTag = 0xC0DE1EA7u;
+
+struct U4 { uint32_t x, y, z, w; };
+
+CVD_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(a, b);
+#else
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+
+// Philox4x32-10 (Salmon et al., SC'11); Random123 known-answer vectors in tests.
+CVD_HD U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = mulhi32(kPhiloxM0, c0), lo0 = kPhiloxM0 * c0;
+    const uint32_t hi1 = mulhi32(kPhiloxM1, c2), lo1 = kPhiloxM1 * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += kPhiloxW0; k1 += kPhiloxW1;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+CVD_HD uint32_t u4_get(const U4& v, uint32_t i) {
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
+// Identity of one simulated sequence.
+struct StreamKey {
+  uint32_t k0, k1;      // seed lo / hi
+  uint32_t tag;         // grid_tag(N, p) or kLearnTag
+};
+
+CVD_HD uint32_t ctr_hi(uint64_t seq_id, uint32_t kind) {
+  return (uint32_t)((seq_id >> 32) & 0xFFFFu) | (kind << 16);
+}
+
+// thr(p) = floor(p * 2^32), p in [0, 1]; flip iff uniform < thr.
+inline uint64_t noise_threshold(double p) { return (uint64_t)(p * 4294967296.0); }
+
+// 32-bit tag of an (N, p) grid point (splitmix64 fold, top bit clear).
+inline uint32_t grid_tag(int64_t N, double p) {
+  uint64_t bits;
+  __builtin_memcpy(&bits, &p, 8);
+  uint64_t x = (uint64_t)N * 0x9E3779B97F4A7C15ull + bits;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)((x ^ (x >> 32)) & 0x7FFFFFFFu);
+}
+
+// Encoder description derived from generator taps (reference convention,
+// viterbi_markov.py:82-106): gmask[j*k + i] bit d = taps[j][i][d] (d <= m);
+// x_i = u_i | (state << 1); out_j = XOR_i parity(gmask[j][i] & x_i);
+// next = (U | state << k) & (2^m - 1).
+constexpr int kMaxK = 4, kMaxN = 8, kMaxM = 8;
+struct CodeDesc {
+  int32_t k, n, m;
+  uint32_t gmask[kMaxN * kMaxK];
+};
+
+CVD_HD uint32_t parity32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popc(x) & 1u;
+#else
+  return (uint32_t)__builtin_popcount(x) & 1u;
+#endif
+}
+
+CVD_HD uint32_t enc_out(const CodeDesc& c, uint32_t s, uint32_t U) {
+  uint32_t o = 0;
+  for (int j = 0; j < c.n; ++j) {
+    uint32_t b = 0;
+    for (int i = 0; i < c.k; ++i) b ^= parity32(c.gmask[j * c.k + i] & (((U >> i) & 1u) | (s << 1)));
+    o |= b << j;
+  }
+  return o;
+}
+
+CVD_HD uint32_t enc_next(const CodeDesc& c, uint32_t s, uint32_t U) {
+  return (U | (s << c.k)) & ((1u << c.m) - 1u);
+}
+
+// Received-word packing in HBM: each 32-bit word holds spw = floor(32 / n)
+// consecutive steps, step i of the word in bits [n*i, n*i + n).  Words are
+// interleaved across sequences: word w of sequence q lives at r[w * pitch + q]
+// (pitch >= number of sequences), so a wave's 64 lanes read 256 contiguous bytes.
+CVD_HD int steps_per_word(int n) { return 32 / n; }
+
+}  // namespace cvd

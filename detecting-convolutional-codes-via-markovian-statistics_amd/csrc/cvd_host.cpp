@@ -1,0 +1,581 @@
+// Host-side native setup behind the C-ABI: code algebra, Eq. 4-5 step on the
+// host, BFS state enumeration, the P̂1 learning chain, T_ref(1/2), the row
+// tables and the explicit-path hash.  None of this is the hot path (the trial
+// loop runs in cvd_kernels.hip); it is the analogue of the reference's table
+// construction (viterbi_markov.py:118-230, Pd_plotter.py:123-169).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/cvd.h"
+#include "cvd_internal.h"
+
+using namespace cvd;
+
+static thread_local std::string g_err;
+void cvd::set_error(const std::string& msg) { g_err = msg; }
+
+#define CVD_TRY try {
+#define CVD_CATCH                                          \
+  }                                                        \
+  catch (const std::bad_alloc&) {                          \
+    set_error("out of host memory");                       \
+    return CVD_E_CAPACITY;                                 \
+  }                                                        \
+  catch (const std::exception& e) {                        \
+    set_error(std::string("internal error: ") + e.what()); \
+    return CVD_E_INVALID;                                  \
+  }
+
+extern "C" int cvd_version(void) { return CVD_ABI_VERSION; }
+extern "C" const char* cvd_last_error(void) { return g_err.c_str(); }
+extern "C" uint32_t cvd_grid_tag(int64_t N, double p) { return grid_tag(N, p); }
+
+// ───────────────────────────── code algebra ─────────────────────────────────
+
+namespace {
+
+struct Tabs {
+  int m, k, n, M, K, R;
+  std::vector<uint8_t> out;   // [M][K] output word
+  std::vector<uint16_t> nxt;  // [M][K]
+};
+
+int parse_code(const cvd_code* c, CodeDesc& d) {
+  if (!c || !c->taps) { set_error("null code"); return CVD_E_INVALID; }
+  if (c->k < 1 || c->k > kMaxK || c->n < 1 || c->n > kMaxN || c->m < 1 || c->m > kMaxM) {
+    set_error("code shape out of range (1<=k<=4, 1<=n<=8, 1<=m<=8)");
+    return CVD_E_INVALID;
+  }
+  d.k = c->k; d.n = c->n; d.m = c->m;
+  std::memset(d.gmask, 0, sizeof(d.gmask));
+  const int L = c->m + 1;
+  for (int j = 0; j < c->n; ++j)
+    for (int i = 0; i < c->k; ++i) {
+      uint32_t g = 0;
+      for (int t = 0; t < L; ++t) {
+        uint8_t b = c->taps[(j * c->k + i) * L + t];
+        if (b > 1) { set_error("taps must be 0/1"); return CVD_E_INVALID; }
+        g |= (uint32_t)b << t;   // taps[d] multiplies x[d]: d=0 input bit, d>=1 state bit d-1
+      }
+      d.gmask[j * c->k + i] = g;
+    }
+  return CVD_OK;
+}
+
+Tabs make_tabs(const CodeDesc& d) {
+  Tabs T;
+  T.m = d.m; T.k = d.k; T.n = d.n; T.M = 1 << d.m; T.K = 1 << d.k; T.R = 1 << d.n;
+  T.out.resize((size_t)T.M * T.K);
+  T.nxt.resize((size_t)T.M * T.K);
+  for (int s = 0; s < T.M; ++s)
+    for (int U = 0; U < T.K; ++U) {
+      T.out[s * T.K + U] = (uint8_t)enc_out(d, s, U);
+      T.nxt[s * T.K + U] = (uint16_t)enc_next(d, s, U);
+    }
+  return T;
+}
+
+// Eq. 4-5 on the host (viterbi_markov.py:139-159).
+inline void step_host(const Tabs& T, const uint8_t* D, uint32_t r, uint8_t* out) {
+  uint8_t best[256];
+  std::memset(best, 0xFF, (size_t)T.M);
+  for (int s = 0; s < T.M; ++s) {
+    const int ds = D[s];
+    for (int U = 0; U < T.K; ++U) {
+      const int v = ds + __builtin_popcount((unsigned)(T.out[s * T.K + U] ^ r));
+      uint8_t& b = best[T.nxt[s * T.K + U]];
+      if (v < b) b = (uint8_t)v;
+    }
+  }
+  uint8_t mn = 255;
+  for (int i = 0; i < T.M; ++i) mn = std::min(mn, best[i]);
+  for (int i = 0; i < T.M; ++i) out[i] = (uint8_t)(best[i] - mn);
+}
+
+// Open-addressing map from metric vectors (M bytes) to row indices.
+struct StateMap {
+  int M;
+  std::vector<uint8_t>* store;  // rows of M bytes
+  std::vector<int32_t> slots;
+  uint64_t mask = 0;
+  int64_t count = 0;
+  StateMap(int M_, std::vector<uint8_t>* st) : M(M_), store(st) { rehash(1024); }
+  static uint64_t hb(const uint8_t* p, int M) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int i = 0; i < M; i += 8) {
+      uint64_t w = 0;
+      std::memcpy(&w, p + i, (size_t)std::min(8, M - i));
+      h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+      h ^= h >> 31;
+    }
+    return h;
+  }
+  void rehash(uint64_t cap) {
+    slots.assign(cap, -1);
+    mask = cap - 1;
+    for (int64_t i = 0; i < count; ++i) {
+      uint64_t h = hb(store->data() + (size_t)i * M, M) & mask;
+      while (slots[h] >= 0) h = (h + 1) & mask;
+      slots[h] = (int32_t)i;
+    }
+  }
+  int64_t find(const uint8_t* key) const {
+    uint64_t h = hb(key, M) & mask;
+    while (true) {
+      int32_t v = slots[h];
+      if (v < 0) return -1;
+      if (!std::memcmp(store->data() + (size_t)v * M, key, (size_t)M)) return v;
+      h = (h + 1) & mask;
+    }
+  }
+  // returns index; inserted=true if new (appended to store)
+  int64_t insert(const uint8_t* key, bool& inserted) {
+    int64_t f = find(key);
+    if (f >= 0) { inserted = false; return f; }
+    if ((uint64_t)(count + 1) * 2 > mask + 1) rehash((mask + 1) * 2);
+    store->insert(store->end(), key, key + M);
+    uint64_t h = hb(key, M) & mask;
+    while (slots[h] >= 0) h = (h + 1) & mask;
+    slots[h] = (int32_t)count;
+    inserted = true;
+    return count++;
+  }
+};
+
+// BFS from D_0 = 0 over all 2^n received words (viterbi_markov.py:166-195):
+// index = discovery order, successors in received-word order.
+int bfs(const Tabs& T, int64_t cap, std::vector<uint8_t>& states, std::vector<int32_t>& next,
+        int64_t& S) {
+  states.clear();
+  next.clear();
+  StateMap map(T.M, &states);
+  std::vector<uint8_t> zero((size_t)T.M, 0), nb((size_t)T.M);
+  bool ins;
+  map.insert(zero.data(), ins);
+  int64_t head = 0;
+  while (head < map.count) {
+    next.resize((size_t)(head + 1) * T.R);
+    // received words in itertools.product order (viterbi_markov.py:175): the
+    // LAST output bit varies fastest, i.e. bit-reversed integer order.
+    for (int i = 0; i < T.R; ++i) {
+      uint32_t r = 0;
+      for (int j = 0; j < T.n; ++j) r |= ((uint32_t)(i >> (T.n - 1 - j)) & 1u) << j;
+      step_host(T, states.data() + (size_t)head * T.M, r, nb.data());
+      int64_t j = map.insert(nb.data(), ins);
+      if (map.count > cap) { S = map.count; return CVD_E_CAPACITY; }
+      next[(size_t)head * T.R + r] = (int32_t)j;
+    }
+    ++head;
+  }
+  S = map.count;
+  return CVD_OK;
+}
+
+// The build's simulator spec (oracle/philox.py) on the host: received words of
+// one sequence, encoder `enc`, BSC(thr).
+struct HostStream {
+  const CodeDesc& enc;
+  const Tabs& T;
+  StreamKey key;
+  uint64_t seq_id;
+  uint64_t thr;
+  bool random_input;
+  uint32_t s = 0;
+  int64_t nblk = -1, iblk = -1;
+  U4 nval{}, ival{};
+  HostStream(const CodeDesc& e, const Tabs& t, uint64_t seed, uint32_t tag, uint64_t sid,
+             double p, bool ri)
+      : enc(e), T(t), key{(uint32_t)seed, (uint32_t)(seed >> 32), tag}, seq_id(sid),
+        thr(noise_threshold(p)), random_input(ri) {}
+  uint32_t noise_u(int64_t g) {
+    const int64_t b = g >> 2;
+    if (b != nblk) {
+      nval = philox((uint32_t)b, (uint32_t)seq_id, ctr_hi(seq_id, kKindNoise), key.tag, key.k0, key.k1);
+      nblk = b;
+    }
+    return u4_get(nval, (uint32_t)(g & 3));
+  }
+  uint32_t input_bit(int64_t bi) {
+    const int64_t b = bi >> 7;
+    if (b != iblk) {
+      ival = philox((uint32_t)b, (uint32_t)seq_id, ctr_hi(seq_id, kKindInput), key.tag, key.k0, key.k1);
+      iblk = b;
+    }
+    return (u4_get(ival, (uint32_t)((bi >> 5) & 3)) >> (bi & 31)) & 1u;
+  }
+  uint32_t next_word(int64_t t) {
+    uint32_t U = 0;
+    if (random_input)
+      for (int i = 0; i < T.k; ++i) U |= input_bit(t * T.k + i) << i;
+    uint32_t r = T.out[s * T.K + U];
+    s = T.nxt[s * T.K + U];
+    for (int j = 0; j < T.n; ++j) r ^= (uint32_t)((uint64_t)noise_u(t * T.n + j) < thr) << j;
+    return r;
+  }
+};
+
+// numpy's float64 add.reduce along a contiguous axis: 0 + pairwise_sum(row)
+// (8 accumulators, 128-element blocks; verified against numpy 2.2 in tests).
+// The row is virtual: lam everywhere except `pos` (ascending) where it is val.
+struct VirtualRow {
+  double lam;
+  const std::vector<std::pair<int64_t, double>>* sp;
+  std::unordered_map<int64_t, double>* memo;
+  double at(int64_t j) const {
+    auto it = std::lower_bound(sp->begin(), sp->end(), std::make_pair(j, -1e308));
+    if (it != sp->end() && it->first == j) return it->second;
+    return lam;
+  }
+  bool has_special(int64_t off, int64_t n) const {
+    auto it = std::lower_bound(sp->begin(), sp->end(), std::make_pair(off, -1e308));
+    return it != sp->end() && it->first < off + n;
+  }
+  double leaf(int64_t off, int64_t n) const {
+    if (n < 8) {
+      double res = 0.;
+      for (int64_t i = 0; i < n; ++i) res += at(off + i);
+      return res;
+    }
+    double r[8];
+    for (int e = 0; e < 8; ++e) r[e] = at(off + e);
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int e = 0; e < 8; ++e) r[e] += at(off + i + e);
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += at(off + i);
+    return res;
+  }
+  double pw(int64_t off, int64_t n) const {
+    if (!has_special(off, n)) {
+      auto it = memo->find(n);
+      if (it != memo->end()) return it->second;
+      double v = (n <= 128) ? leaf(off, n) : 0.0;
+      if (n > 128) {
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        v = pw(off, n2) + pw(off + n2, n - n2);
+      }
+      (*memo)[n] = v;
+      return v;
+    }
+    if (n <= 128) return leaf(off, n);
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw(off, n2) + pw(off + n2, n - n2);
+  }
+};
+
+double ltref_value(int c, int R) { return std::log(std::max((double)c / (double)R, 1e-300)); }
+
+// Row of P̂1 (Pd_plotter.py:166-167) for one state: counts per successor
+// index; returns log P for each received word.
+double p1_row(int64_t S, double lam, std::unordered_map<int64_t, double>& memo,
+              const int64_t* succ /*[R], -1 = unvisited successor*/, const int64_t* cnt_r /*[R]*/,
+              int R, double* logp_out, std::vector<std::pair<int64_t, double>>* nz = nullptr) {
+  std::vector<std::pair<int64_t, double>> sp;
+  for (int r = 0; r < R; ++r) {
+    if (succ[r] < 0 || cnt_r[r] == 0) continue;
+    bool found = false;
+    for (auto& e : sp)
+      if (e.first == succ[r]) { e.second += (double)cnt_r[r]; found = true; }
+    if (!found) sp.emplace_back(succ[r], (double)cnt_r[r]);
+  }
+  std::sort(sp.begin(), sp.end());
+  for (auto& e : sp) e.second = e.second + lam;   // counts + laplace (elementwise)
+  VirtualRow vr{lam, &sp, &memo};
+  const double rowsum = 0.0 + vr.pw(0, S);
+  for (int r = 0; r < R; ++r) {
+    double v = lam;
+    if (succ[r] >= 0)
+      for (auto& e : sp)
+        if (e.first == succ[r]) v = e.second;
+    logp_out[r] = std::log(std::max(v / rowsum, 1e-300));
+  }
+  if (nz) *nz = sp;
+  return rowsum;
+}
+
+}  // namespace
+
+void cvd::pack_nibbles(const uint8_t* D, int M, uint32_t* out) {
+  const int nw = M >= 8 ? M / 8 : 1;
+  for (int w = 0; w < nw; ++w) out[w] = 0;
+  for (int s = 0; s < M; ++s) out[s / 8] |= (uint32_t)(D[s] & 15) << (4 * (s % 8));
+}
+
+// ───────────────────────────── ABI: algebra ─────────────────────────────────
+
+extern "C" int cvd_code_tables(const cvd_code* code, int32_t* out_sym, int32_t* next_state) {
+  CVD_TRY
+  CodeDesc d;
+  int rc = parse_code(code, d);
+  if (rc) return rc;
+  Tabs T = make_tabs(d);
+  for (int i = 0; i < T.M * T.K; ++i) {
+    if (out_sym) out_sym[i] = T.out[i];
+    if (next_state) next_state[i] = T.nxt[i];
+  }
+  return CVD_OK;
+  CVD_CATCH
+}
+
+extern "C" int cvd_metric_step(const cvd_code* dec, const uint8_t* D_prev, int32_t r, uint8_t* D_out) {
+  CVD_TRY
+  CodeDesc d;
+  int rc = parse_code(dec, d);
+  if (rc) return rc;
+  if (!D_prev || !D_out || r < 0 || r >= (1 << d.n)) { set_error("bad step arguments"); return CVD_E_INVALID; }
+  Tabs T = make_tabs(d);
+  step_host(T, D_prev, (uint32_t)r, D_out);
+  return CVD_OK;
+  CVD_CATCH
+}
+
+extern "C" int cvd_enumerate(const cvd_code* dec, int64_t cap, int64_t* S_out, uint8_t* states_out,
+                             int32_t* next_out) {
+  CVD_TRY
+  CodeDesc d;
+  int rc = parse_code(dec, d);
+  if (rc) return rc;
+  Tabs T = make_tabs(d);
+  std::vector<uint8_t> states;
+  std::vector<int32_t> next;
+  int64_t S = 0;
+  rc = bfs(T, cap, states, next, S);
+  if (S_out) *S_out = S;
+  if (rc) { set_error("state enumeration exceeded cap"); return rc; }
+  if (states_out) std::memcpy(states_out, states.data(), states.size());
+  if (next_out) std::memcpy(next_out, next.data(), next.size() * sizeof(int32_t));
+  return CVD_OK;
+  CVD_CATCH
+}
+
+// ───────────────────────────── ABI: model ───────────────────────────────────
+
+namespace {
+
+void build_hash(cvd_model& Mo) {
+  const int m = Mo.dec.m, M = 1 << m, R = 1 << Mo.dec.n, nw = nib_words(m);
+  int64_t cap = 64;
+  while (cap < 2 * Mo.n_rows) cap <<= 1;
+  Mo.hcap = cap;
+  Mo.h_fp.assign((size_t)cap, 0u);
+  const int kw_pad = rec_key_words(m);
+  Mo.h_rw = rec_words(m, Mo.dec.n);
+  Mo.h_rec.assign((size_t)cap * Mo.h_rw, 0u);
+  Mo.max_probe = 0;
+  std::vector<uint32_t> kw((size_t)nw);
+  for (int64_t i = 0; i < Mo.n_rows; ++i) {
+    pack_nibbles(Mo.keys.data() + (size_t)i * M, M, kw.data());
+    uint32_t h1, h2;
+    key_hash(kw.data(), nw, h1, h2);
+    uint64_t slot = h1 & (uint64_t)(cap - 1);
+    int probe = 0;
+    while (Mo.h_fp[slot]) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
+    Mo.max_probe = std::max(Mo.max_probe, probe);
+    Mo.h_fp[slot] = h2 | 1u;
+    uint32_t* rec = Mo.h_rec.data() + slot * Mo.h_rw;
+    for (int w = 0; w < nw; ++w) rec[w] = kw[w];
+    std::memcpy(rec + kw_pad, Mo.logp1.data() + (size_t)i * R, sizeof(double) * R);
+  }
+}
+
+void build_bmp(cvd_model& Mo, const Tabs& T) {
+  if (!explicit_supported(T.m, T.k, T.n)) return;
+  const int QP = T.R / 2;
+  Mo.bmp.assign((size_t)QP * T.M * T.K, 0u);
+  for (int qp = 0; qp < QP; ++qp)
+    for (int ns = 0; ns < T.M; ++ns)
+      for (int b = 0; b < T.K; ++b) {
+        const int pred = (ns >> T.k) | (b << (T.m - T.k));
+        const int U = ns & (T.K - 1);
+        const uint32_t o = T.out[pred * T.K + U];
+        const uint32_t b0 = __builtin_popcount(o ^ (uint32_t)(2 * qp));
+        const uint32_t b1 = __builtin_popcount(o ^ (uint32_t)(2 * qp + 1));
+        Mo.bmp[((size_t)qp * T.M + ns) * T.K + b] = b0 | (b1 << 16);
+      }
+}
+
+}  // namespace
+
+bool cvd::explicit_supported(int m, int k, int n) {
+  // nibble storage of un-normalised metrics: D <= ceil(m/k)*n, plus one branch (<= n)
+  const int L = (m + k - 1) / k;
+  const bool shape = (m == 2 && k == 1 && n == 2) || (m == 3 && k == 1 && n == 2) ||
+                     (m == 4 && k == 1 && n == 2) || (m == 5 && k == 1 && n == 2) ||
+                     (m == 6 && k == 1 && n == 2) || (m == 4 && k == 2 && n == 3);
+  return shape && (L + 1) * n <= 15;
+}
+
+extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm, cvd_model** out) {
+  CVD_TRY
+  if (!prm || !out) { set_error("null argument"); return CVD_E_INVALID; }
+  *out = nullptr;
+  if (!(prm->p >= 0.0 && prm->p <= 1.0)) { set_error("p must lie in [0, 1]"); return CVD_E_INVALID; }
+  if (!(prm->laplace >= 0.0) || prm->learn_burn < 0) { set_error("bad learning parameters"); return CVD_E_INVALID; }
+  std::unique_ptr<cvd_model> Mo(new cvd_model());
+  int rc = parse_code(dec, Mo->dec);
+  if (rc) return rc;
+  Tabs T = make_tabs(Mo->dec);
+  const int M = T.M, R = T.R;
+  Mo->laplace = prm->laplace;
+  Mo->ltref.resize((size_t)R + 1);
+  for (int c = 0; c <= R; ++c) Mo->ltref[c] = ltref_value(c, R);
+  const uint64_t seed = prm->seed;
+
+  std::vector<uint8_t> states;
+  std::vector<int32_t> next;
+  int64_t S = 0;
+  const int64_t cap = prm->enum_cap > 0 ? prm->enum_cap : 0;
+  rc = cap > 0 ? bfs(T, cap, states, next, S) : CVD_E_CAPACITY;
+  std::unordered_map<int64_t, double> memo;
+
+  if (rc == CVD_OK) {
+    // ── dense model: the reference's exact semantics (Pd_plotter.py:123-169) ──
+    Mo->kind = 0;
+    Mo->S = S;
+    const int64_t L = prm->learn_len < 0 ? std::max<int64_t>(5000, 200 * S) : prm->learn_len;
+    Mo->learn_len_eff = L;
+    std::vector<int64_t> cnt((size_t)S * R, 0);
+    HostStream hs(Mo->dec, T, seed, kLearnTag, 0, prm->p, true);
+    int64_t i = 0;   // D_0 = 0 is BFS index 0
+    for (int64_t t = 0; t < L; ++t) {
+      const uint32_t r = hs.next_word(t);
+      if (t >= prm->learn_burn) cnt[(size_t)i * R + r]++;
+      i = next[(size_t)i * R + r];
+    }
+    Mo->n_rows = S;
+    Mo->keys = std::move(states);
+    Mo->logp1.assign((size_t)S * R, 0.0);
+    Mo->rec.assign((size_t)S * R, 0u);
+    std::vector<int64_t> succ((size_t)R);
+    std::vector<std::pair<int64_t, double>> nz;
+    Mo->rowsum.assign((size_t)S, 0.0);
+    for (int64_t s = 0; s < S; ++s) {
+      for (int r = 0; r < R; ++r) succ[r] = next[(size_t)s * R + r];
+      Mo->rowsum[(size_t)s] = p1_row(S, prm->laplace, memo, succ.data(), cnt.data() + (size_t)s * R, R,
+                                     Mo->logp1.data() + (size_t)s * R, &nz);
+      for (auto& e : nz) Mo->p1_nz.push_back({s, e.first, e.second});
+      for (int r = 0; r < R; ++r) {
+        int c = 0;
+        for (int q = 0; q < R; ++q) c += succ[q] == succ[r];
+        Mo->rec[(size_t)s * R + r] = ((uint32_t)succ[r] << 4) | (uint32_t)c;
+      }
+    }
+    {
+      std::vector<int64_t> none((size_t)R, -1), zc((size_t)R, 0);
+      std::vector<double> lp((size_t)R);
+      p1_row(S, prm->laplace, memo, none.data(), zc.data(), R, lp.data());
+      Mo->logp1_unseen = lp[0];
+    }
+  } else if (rc == CVD_E_CAPACITY) {
+    // ── sparse model: rows = states visited by the learning chain ──
+    // The reference's semantics need the full BFS index (Pd_plotter.py:136-139,
+    // 166-167), infeasible here (m = 6: > 2e8 states).  Declared policy
+    // (deviation D3): the state set is the chain's visited states
+    // D_0..D_L in first-visit order, S = their number, unvisited rows are the
+    // all-zero-count row λ / (S λ).
+    Mo->kind = 1;
+    const int64_t L = prm->learn_len >= 0 ? prm->learn_len
+                                          : (prm->default_learn_len > 0 ? prm->default_learn_len : 1000000);
+    Mo->learn_len_eff = L;
+    std::vector<uint8_t> keys;
+    StateMap map(M, &keys);
+    std::vector<int64_t> cnt;
+    std::vector<uint8_t> D((size_t)M, 0), Dn((size_t)M);
+    bool ins;
+    int64_t i = map.insert(D.data(), ins);
+    cnt.resize((size_t)R, 0);
+    HostStream hs(Mo->dec, T, seed, kLearnTag, 0, prm->p, true);
+    for (int64_t t = 0; t < L; ++t) {
+      const uint32_t r = hs.next_word(t);
+      if (t >= prm->learn_burn) cnt[(size_t)i * R + r]++;
+      step_host(T, D.data(), r, Dn.data());
+      int64_t j = map.insert(Dn.data(), ins);
+      if (ins) cnt.resize((size_t)map.count * R, 0);
+      std::swap(D, Dn);
+      i = j;
+    }
+    S = map.count;
+    Mo->S = S;
+    Mo->n_rows = S;
+    Mo->logp1.assign((size_t)S * R, 0.0);
+    std::vector<int64_t> succ((size_t)R);
+    for (int64_t s = 0; s < S; ++s) {
+      for (int r = 0; r < R; ++r) {
+        step_host(T, keys.data() + (size_t)s * M, (uint32_t)r, Dn.data());
+        succ[r] = map.find(Dn.data());
+      }
+      p1_row(S, prm->laplace, memo, succ.data(), cnt.data() + (size_t)s * R, R,
+             Mo->logp1.data() + (size_t)s * R);
+    }
+    Mo->keys = std::move(keys);
+    std::vector<int64_t> none((size_t)R, -1), zc((size_t)R, 0);
+    std::vector<double> lp((size_t)R);
+    p1_row(S, prm->laplace, memo, none.data(), zc.data(), R, lp.data());
+    Mo->logp1_unseen = lp[0];
+  } else {
+    return rc;
+  }
+  if (explicit_supported(T.m, T.k, T.n)) {
+    build_hash(*Mo);
+    build_bmp(*Mo, T);
+  }
+  *out = Mo.release();
+  return CVD_OK;
+  CVD_CATCH
+}
+
+extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
+  if (!Mo || !info) { set_error("null argument"); return CVD_E_INVALID; }
+  info->kind = Mo->kind;
+  info->k = Mo->dec.k; info->n = Mo->dec.n; info->m = Mo->dec.m;
+  info->S = Mo->S;
+  info->n_rows = Mo->n_rows;
+  info->learn_len_eff = Mo->learn_len_eff;
+  info->hash_capacity = Mo->hcap;
+  info->max_probe = Mo->max_probe;
+  info->device = Mo->device;
+  info->logp1_unseen = Mo->logp1_unseen;
+  return CVD_OK;
+}
+
+extern "C" int cvd_model_dense_P1(const cvd_model* Mo, double* P_out, int64_t S) {
+  CVD_TRY
+  if (!Mo || !P_out) { set_error("null argument"); return CVD_E_INVALID; }
+  if (Mo->kind != 0 || S != Mo->S) { set_error("dense P1 only for dense models with matching S"); return CVD_E_INVALID; }
+  for (int64_t i = 0; i < S; ++i) {
+    const double base = Mo->laplace / Mo->rowsum[(size_t)i];
+    for (int64_t j = 0; j < S; ++j) P_out[(size_t)i * S + j] = base;
+  }
+  for (const auto& e : Mo->p1_nz)
+    P_out[(size_t)e.row * S + e.col] = e.val / Mo->rowsum[(size_t)e.row];
+  return CVD_OK;
+  CVD_CATCH
+}
+
+extern "C" int cvd_model_rows(const cvd_model* Mo, double* logp1_out, uint8_t* keys_out, int64_t n_rows) {
+  if (!Mo) { set_error("null model"); return CVD_E_INVALID; }
+  if (n_rows != Mo->n_rows) { set_error("n_rows mismatch"); return CVD_E_INVALID; }
+  const int R = 1 << Mo->dec.n, M = 1 << Mo->dec.m;
+  if (logp1_out) std::memcpy(logp1_out, Mo->logp1.data(), (size_t)n_rows * R * sizeof(double));
+  if (keys_out) std::memcpy(keys_out, Mo->keys.data(), (size_t)n_rows * M);
+  return CVD_OK;
+}
+
+extern "C" int cvd_model_upload(cvd_model* Mo, int device) {
+  if (!Mo) { set_error("null model"); return CVD_E_INVALID; }
+  return upload_model(*Mo, device);
+}
+
+extern "C" void cvd_model_destroy(cvd_model* Mo) {
+  if (!Mo) return;
+  free_model_device(*Mo);
+  delete Mo;
+}

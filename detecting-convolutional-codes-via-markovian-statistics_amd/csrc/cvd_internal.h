@@ -1,0 +1,85 @@
+// Internal structures shared by the host setup (cvd_host.cpp) and the HIP
+// kernels/launchers (cvd_kernels.hip).  Not part of the ABI.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "cvd_common.h"
+
+struct cvd_model {
+  cvd::CodeDesc dec;          // decoder trellis (G1; Pd_plotter.py:188 "decoder is fixed to H1")
+  int32_t kind = 0;           // 0 dense (BFS index, reference-exact), 1 sparse (learned states)
+  int64_t S = 0;              // Laplace denominator state count
+  int64_t learn_len_eff = 0;
+  double laplace = 1.0;
+  double logp1_unseen = 0.0;  // log P̂1 of an unvisited row: log(λ / (S λ))
+  std::vector<double> ltref;  // ltref[c] = log(max(c / 2^n, 1e-300)), c = 0..2^n
+
+  // rows (dense: BFS order; sparse: first-visit order of the learning chain)
+  int64_t n_rows = 0;
+  std::vector<uint8_t> keys;      // [n_rows][2^m] metric bytes
+  std::vector<double> logp1;      // [n_rows][2^n]
+  std::vector<uint32_t> rec;      // dense only: [S][2^n] = next_index << 4 | c
+  struct NZ { int64_t row, col; double val; };
+  std::vector<double> rowsum;     // dense only: numpy row sums of counts + λ
+  std::vector<NZ> p1_nz;          // dense only: entries with counts (value = C + λ)
+
+  // explicit-path hash over nibble-packed keys
+  int64_t hcap = 0;               // power of two, 0 = none
+  int32_t max_probe = 0;
+  std::vector<uint32_t> h_fp;     // [hcap] fingerprint | 1, 0 = empty
+  int32_t h_rw = 0;               // record stride in dwords: key (NW, padded to even) + 2^n doubles, 16-B multiple
+  std::vector<uint32_t> h_rec;    // [hcap][h_rw]
+  std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
+
+  // device copies
+  int device = -1;
+  uint32_t* d_rec = nullptr;
+  double* d_logp1 = nullptr;
+  double* d_ltref = nullptr;
+  uint32_t* d_fp = nullptr;
+  uint32_t* d_hrec = nullptr;
+  uint32_t* d_bmp = nullptr;
+};
+
+namespace cvd {
+
+void set_error(const std::string& msg);
+inline int nib_words(int m) { return (1 << m) >= 8 ? (1 << m) / 8 : 1; }
+inline int rec_key_words(int m) { return (nib_words(m) + 1) & ~1; }   // doubles start 8-B aligned
+inline int rec_words(int m, int n) { return (rec_key_words(m) + 2 * (1 << n) + 3) & ~3; }
+
+// Nibble packing of a metric vector: state s in nibble s (word s / 8, bits 4*(s % 8)).
+void pack_nibbles(const uint8_t* D, int M, uint32_t* out);
+
+// 32-bit hash pair of a nibble-packed key; must match the device version.
+CVD_HD void key_hash(const uint32_t* w, int nw, uint32_t& h1, uint32_t& h2) {
+  uint32_t a = 0x9E3779B9u ^ (uint32_t)nw, b = 0x7F4A7C15u;
+  for (int i = 0; i < nw; ++i) {
+    a = (a ^ w[i]) * 0x85EBCA6Bu;
+    a ^= a >> 15;
+    b = (b + w[i]) * 0xC2B2AE35u;
+    b ^= b >> 13;
+  }
+  a ^= a >> 16;
+  b = (b ^ (b >> 16)) * 0x27D4EB2Fu;
+  h1 = a;
+  h2 = b ^ (b >> 15);
+}
+
+// kernel launchers (cvd_kernels.hip)
+int launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, uint64_t thr,
+                    int64_t N, int random_input, int64_t seq_base, int64_t seq_stride,
+                    uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream);
+int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
+                        int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream);
+int launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
+                           int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
+                           void* stream);
+int upload_model(cvd_model& M, int device);
+void free_model_device(cvd_model& M);
+bool explicit_supported(int m, int k, int n);
+
+}  // namespace cvd

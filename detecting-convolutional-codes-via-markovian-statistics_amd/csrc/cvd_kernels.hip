@@ -1,0 +1,568 @@
+// HIP kernels for gfx950 (MI355X): the Monte-Carlo hot path of the reference
+// (Pd_plotter.py:198-233 with the missing simulator of Pd_plotter.py:149/212/219,
+// the Eq. 4-5 recursion of viterbi_markov.py:139-159 and the likelihood
+// accumulation of Pd_plotter.py:106-116).
+//
+//   gen_kernel               encoder + BSC(p) -> bit-packed received words in HBM
+//                            (one sequence per lane, words interleaved across lanes)
+//   detect_table_kernel      enumerated-state automaton: per step one (next, c)
+//                            record + one log P̂1 row entry; tables in LDS when they fit
+//   detect_explicit_kernel   explicit 2^m relative-metric vector per lane (nibble
+//                            packed), Eq. 4-5 for ALL 2^n received words with packed
+//                            16-bit VALU ops (two received words per instruction), T_ref
+//                            count by exact comparison, P̂1 row from a hashed table
+//
+// All sums are sequential fp64 additions in t order (no FMA, no reassociation),
+// so every per-sequence sum and decision is bit-identical to the reference's
+// `logp += math.log(pij)` loop.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+
+#include "../../include/cvd.h"
+#include "cvd_common.h"
+#include "cvd_internal.h"
+
+using namespace cvd;
+
+#define HIP_CHECK(x)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      set_error(std::string("HIP error '") + hipGetErrorString(e_) + "' at " #x);          \
+      return CVD_E_HIP;                                                                   \
+    }                                                                                     \
+  } while (0)
+
+namespace {
+
+constexpr int kBlock = 256;
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
+__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// Wave-level success counting: one 64-bit atomic per wave and hypothesis.
+__device__ __forceinline__ void count_decisions(bool valid, bool is_h1, double lp, double lr,
+                                                int64_t* counts) {
+  const bool s1 = valid && is_h1 && (lp > lr);     // Pd_plotter.py:215
+  const bool s2 = valid && !is_h1 && (lp <= lr);   // Pd_plotter.py:222
+  const unsigned long long b1 = __ballot(s1), b2 = __ballot(s2);
+  if ((threadIdx.x & 63) == 0) {
+    if (b1) atomicAdd(reinterpret_cast<unsigned long long*>(counts), (unsigned long long)__popcll(b1));
+    if (b2) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), (unsigned long long)__popcll(b2));
+  }
+}
+
+// ───────────────────────────── generator ────────────────────────────────────
+
+struct GenArgs {
+  CodeDesc enc;
+  uint32_t k0, k1, tag, thr_lo;
+  int32_t thr_all, random_input;
+  int64_t N, seq_base, seq_stride, pitch, q0, count;
+  uint32_t* r;
+};
+
+__global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
+  const int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (li >= a.count) return;
+  const int64_t q = a.q0 + li;
+  const uint64_t sid = (uint64_t)(a.seq_base + li * a.seq_stride);
+  const uint32_t slo = (uint32_t)sid, nhi = ctr_hi(sid, kKindNoise), ihi = ctr_hi(sid, kKindInput);
+  const int n = a.enc.n, k = a.enc.k, spw = 32 / n;
+  const uint32_t kmask = (1u << k) - 1u;
+  const int64_t nwords = (a.N + spw - 1) / spw;
+  uint32_t s = 0;
+  int64_t cblk = -1;
+  U4 cval{0, 0, 0, 0};
+  for (int64_t w = 0; w < nwords; ++w) {
+    const int64_t t0 = w * spw;
+    const int ns = (int)min((int64_t)spw, a.N - t0);
+    // BSC flips of the word's n*ns code bits (noise uniform g = t*n + j)
+    uint32_t nmask = 0;
+    const int64_t g0 = t0 * n, g1 = g0 + (int64_t)ns * n;
+    for (int64_t b = g0 >> 2; b <= ((g1 - 1) >> 2); ++b) {
+      const U4 x = philox((uint32_t)b, slo, nhi, a.tag, a.k0, a.k1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t g = 4 * b + e;
+        const uint32_t u = u4_get(x, e);
+        const uint32_t flip = a.thr_all ? 1u : (u < a.thr_lo ? 1u : 0u);
+        if (g >= g0 && g < g1) nmask |= flip << (uint32_t)(g - g0);
+      }
+    }
+    // encoder input bits [t0*k, (t0+ns)*k) of the input stream
+    uint32_t ib = 0;
+    if (a.random_input) {
+      const int64_t b0 = t0 * k;
+      const int64_t W = b0 >> 5;
+      const uint32_t off = (uint32_t)(b0 & 31);
+      uint32_t wv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t Wh = W + h;
+        if (h == 1 && off + (uint32_t)(ns * k) <= 32u) { wv[1] = 0; break; }
+        if ((Wh >> 2) != cblk) {
+          cblk = Wh >> 2;
+          cval = philox((uint32_t)cblk, slo, ihi, a.tag, a.k0, a.k1);
+        }
+        wv[h] = u4_get(cval, (uint32_t)(Wh & 3));
+      }
+      ib = off ? ((wv[0] >> off) | (wv[1] << (32u - off))) : wv[0];
+    }
+    uint32_t word = 0;
+    for (int i = 0; i < ns; ++i) {
+      const uint32_t U = (ib >> (uint32_t)(i * k)) & kmask;
+      word |= enc_out(a.enc, s, U) << (uint32_t)(n * i);
+      s = enc_next(a.enc, s, U);
+    }
+    a.r[w * a.pitch + q] = word ^ nmask;
+  }
+}
+
+// ─────────────────────────── table automaton ────────────────────────────────
+
+struct TabArgs {
+  const uint32_t* rec;    // [S][R]: next << 4 | c
+  const double* logp1;    // [S][R]
+  const double* ltref;    // [R + 1]
+  int32_t n;
+  int64_t S, N, nseq, n_h1;
+  const uint32_t* r;
+  double* sums;
+  int64_t* counts;
+};
+
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int R = 1 << a.n;
+  const int64_t SR = a.S * R;
+  const uint32_t* rec = a.rec;
+  const double* lp1 = a.logp1;
+  const double* ltr = a.ltref;
+  if (kLds) {
+    double* s_lp = reinterpret_cast<double*>(smem);
+    double* s_lt = s_lp + SR;
+    uint32_t* s_rec = reinterpret_cast<uint32_t*>(s_lt + R + 1);
+    for (int64_t i = threadIdx.x; i < SR; i += kBlock) { s_lp[i] = a.logp1[i]; s_rec[i] = a.rec[i]; }
+    for (int i = threadIdx.x; i <= R; i += kBlock) s_lt[i] = a.ltref[i];
+    __syncthreads();
+    rec = s_rec; lp1 = s_lp; ltr = s_lt;
+  }
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = q < a.nseq;
+  double lp = 0.0, lr = 0.0;
+  if (valid) {
+    const int spw = 32 / a.n;
+    const uint32_t rmask = (uint32_t)R - 1u;
+    const int64_t nwords = (a.N + spw - 1) / spw;
+    uint32_t st = 0;                     // index of D_0 = 0 (first BFS state)
+    for (int64_t w = 0; w < nwords; ++w) {
+      uint32_t word = a.r[w * a.nseq + q];
+      const int ns = (int)min((int64_t)spw, a.N - w * spw);
+      for (int i = 0; i < ns; ++i) {
+        const uint32_t idx = st * (uint32_t)R + (word & rmask);
+        word >>= a.n;
+        const uint32_t e = rec[idx];
+        lp += lp1[idx];                  // log P̂1[i, j]   (Pd_plotter.py:213)
+        lr += ltr[e & 15u];              // log T_ref[i, j] = log(c / 2^n) (Pd_plotter.py:214)
+        st = e >> 4;
+      }
+    }
+    if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+  }
+  count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
+}
+
+// ────────────────────────── explicit metric path ────────────────────────────
+
+struct ExpArgs {
+  const uint32_t* fp;       // [hcap]
+  const uint32_t* hrec;     // [hcap][RW]
+  const double* ltref;      // [R + 1]
+  const uint32_t* bmp;      // [QP][M][K] packed branch metrics (bm(2qp), bm(2qp+1))
+  uint32_t hmask;
+  int32_t max_probe;
+  double lp_unseen;
+  int64_t N, nseq, n_h1;
+  const uint32_t* r;
+  double* sums;
+  int64_t* counts;
+  uint8_t* trace;
+};
+
+template <int m, int k, int n>
+struct Shape {
+  static constexpr int M = 1 << m, K = 1 << k, R = 1 << n, QP = R / 2;
+  static constexpr int NG = M / 4;                // groups of 4 states (one 16-bit half)
+  static constexpr int NW = M >= 8 ? M / 8 : 1;   // nibble-packed words of a metric vector
+  static constexpr int KW = (NW + 1) & ~1;        // record key words (doubles 8-B aligned)
+  static constexpr int RW = (KW + 2 * R + 3) & ~3;
+  static constexpr int SPW = 32 / n;
+  static_assert(m >= 2 && k <= m && n >= 1, "explicit path shape");
+};
+
+template <int m, int k, int n>
+__device__ __forceinline__ void write_trace(uint8_t* tr, int64_t t, int64_t nseq, int64_t q,
+                                            const uint32_t (&Dw)[Shape<m, k, n>::NW]) {
+  using S = Shape<m, k, n>;
+  uint8_t* o = tr + ((size_t)t * nseq + q) * S::M;
+#pragma unroll
+  for (int s = 0; s < S::M; ++s) o[s] = (uint8_t)((Dw[s >> 3] >> (4 * (s & 7))) & 15u);
+}
+
+template <int m, int k, int n>
+__global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
+  using S = Shape<m, k, n>;
+  __shared__ double s_lt[S::R + 1];
+  if (threadIdx.x <= S::R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  __syncthreads();
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = q < a.nseq;
+  double lp = 0.0, lr = 0.0;
+  if (valid) {
+    uint32_t Dw[S::NW];
+#pragma unroll
+    for (int w = 0; w < S::NW; ++w) Dw[w] = 0u;
+    if (a.trace) write_trace<m, k, n>(a.trace, 0, a.nseq, q, Dw);
+    const int64_t nwords = (a.N + S::SPW - 1) / S::SPW;
+    int64_t t = 0;
+    for (int64_t wi = 0; wi < nwords; ++wi) {
+      uint32_t word = a.r[wi * a.nseq + q];
+      const int ns = (int)min((int64_t)S::SPW, a.N - wi * S::SPW);
+      for (int i = 0; i < ns; ++i) {
+        const uint32_t rr = word & (uint32_t)(S::R - 1);
+        word >>= n;
+        // (1) P̂1 row of D_{t-1}: first probe issued now, resolved after the ACS.
+        uint32_t h1, h2;
+        key_hash(Dw, S::NW, h1, h2);
+        uint32_t slot = h1 & a.hmask;
+        const uint32_t fpv = h2 | 1u;
+        const uint32_t f0 = a.fp[slot];
+        const uint32_t* rec0 = a.hrec + (size_t)slot * S::RW;
+        uint32_t key0[S::NW];
+#pragma unroll
+        for (int w = 0; w < S::NW; ++w) key0[w] = rec0[w];
+        const double l0 = reinterpret_cast<const double*>(rec0 + S::KW)[rr];
+
+        // (2) Eq. 4 for every received word q', two per packed-16 instruction.
+        uint32_t dup[S::M];
+#pragma unroll
+        for (int s = 0; s < S::M; ++s) dup[s] = ((Dw[s >> 3] >> (4 * (s & 7))) & 15u) * 0x10001u;
+        uint32_t P[S::QP][S::NG];
+#pragma unroll
+        for (int qp = 0; qp < S::QP; ++qp) {
+          us2 mu = as_us2(0xFFFFFFFFu);
+#pragma unroll
+          for (int g = 0; g < S::NG; ++g) {
+            uint32_t packed = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int ns_ = 4 * g + e;
+              us2 best;
+#pragma unroll
+              for (int b = 0; b < S::K; ++b) {
+                const int pred = (ns_ >> k) | (b << (m - k));
+                const us2 c = as_us2(dup[pred]) + as_us2(a.bmp[(qp * S::M + ns_) * S::K + b]);
+                best = b == 0 ? c : __builtin_elementwise_min(best, c);
+              }
+              mu = __builtin_elementwise_min(mu, best);
+              packed |= as_u32(best) << (4 * e);
+            }
+            P[qp][g] = packed;
+          }
+          // Eq. 5: subtract the minimum from every nibble of both halves
+          const uint32_t muN = ((uint32_t)mu.x * 0x1111u) | (((uint32_t)mu.y * 0x1111u) << 16);
+#pragma unroll
+          for (int g = 0; g < S::NG; ++g) P[qp][g] -= muN;
+        }
+        // (3) the observed successor D_t and c = #{q' : D_t(q') == D_t(r_t)}
+        const uint32_t qsel = rr >> 1, hsh = (rr & 1u) * 16u;
+        uint32_t obs[S::NG];
+#pragma unroll
+        for (int g = 0; g < S::NG; ++g) {
+          uint32_t x = P[0][g];
+#pragma unroll
+          for (int qp = 1; qp < S::QP; ++qp) x = (qsel == (uint32_t)qp) ? P[qp][g] : x;
+          obs[g] = (x >> hsh) & 0xFFFFu;
+        }
+        uint32_t c = 0;
+#pragma unroll
+        for (int qp = 0; qp < S::QP; ++qp) {
+          uint32_t acc = 0;
+#pragma unroll
+          for (int g = 0; g < S::NG; ++g) acc |= P[qp][g] ^ (obs[g] * 0x10001u);
+          c += ((acc & 0xFFFFu) == 0u) + ((acc >> 16) == 0u);
+        }
+        // (4) resolve the P̂1 lookup (exact key compare; linear probing)
+        double lpv = a.lp_unseen;
+        {
+          bool eq = f0 == fpv;
+#pragma unroll
+          for (int w = 0; w < S::NW; ++w) eq = eq && (key0[w] == Dw[w]);
+          if (eq) {
+            lpv = l0;
+          } else if (f0 != 0u) {
+            for (int pr = 1; pr <= a.max_probe; ++pr) {
+              slot = (slot + 1u) & a.hmask;
+              const uint32_t f = a.fp[slot];
+              if (f == 0u) break;
+              if (f == fpv) {
+                const uint32_t* rc = a.hrec + (size_t)slot * S::RW;
+                bool e2 = true;
+#pragma unroll
+                for (int w = 0; w < S::NW; ++w) e2 = e2 && (rc[w] == Dw[w]);
+                if (e2) { lpv = reinterpret_cast<const double*>(rc + S::KW)[rr]; break; }
+              }
+            }
+          }
+        }
+        lp += lpv;            // Pd_plotter.py:115 with T = P̂1
+        lr += s_lt[c];        // Pd_plotter.py:115 with T = T_ref(1/2) = c / 2^n
+        // (5) D_t becomes the state
+        if (S::NW == 1) {
+          Dw[0] = S::NG == 1 ? obs[0] : (obs[0] | (obs[1] << 16));
+        } else {
+#pragma unroll
+          for (int w = 0; w < S::NW; ++w) Dw[w] = obs[2 * w] | (obs[2 * w + 1] << 16);
+        }
+        ++t;
+        if (a.trace) write_trace<m, k, n>(a.trace, t, a.nseq, q, Dw);
+      }
+    }
+    if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+  }
+  count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
+}
+
+using ExpKernel = void (*)(ExpArgs);
+ExpKernel pick_explicit(int m, int k, int n) {
+  if (k == 1 && n == 2) {
+    switch (m) {
+      case 2: return detect_explicit_kernel<2, 1, 2>;
+      case 3: return detect_explicit_kernel<3, 1, 2>;
+      case 4: return detect_explicit_kernel<4, 1, 2>;
+      case 5: return detect_explicit_kernel<5, 1, 2>;
+      case 6: return detect_explicit_kernel<6, 1, 2>;
+    }
+  }
+  if (m == 4 && k == 2 && n == 3) return detect_explicit_kernel<4, 2, 3>;
+  return nullptr;
+}
+
+int check_device(const cvd_model& M) {
+  if (M.device < 0) { set_error("model not uploaded (cvd_model_upload)"); return CVD_E_STATE; }
+  int cur = -1;
+  HIP_CHECK(hipGetDevice(&cur));
+  if (cur != M.device) { set_error("current device differs from the model's device"); return CVD_E_INVALID; }
+  return CVD_OK;
+}
+
+template <typename T>
+int dev_copy(T*& d, const std::vector<T>& h) {
+  if (h.empty()) return CVD_OK;
+  HIP_CHECK(hipMalloc(&d, h.size() * sizeof(T)));
+  HIP_CHECK(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return CVD_OK;
+}
+
+}  // namespace
+
+// ───────────────────────────── launchers ─────────────────────────────────────
+
+int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, uint64_t thr,
+                         int64_t N, int random_input, int64_t seq_base, int64_t seq_stride,
+                         uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream) {
+  if (count <= 0 || N <= 0) return CVD_OK;
+  GenArgs a;
+  a.enc = enc; a.k0 = k0; a.k1 = k1; a.tag = tag;
+  a.thr_all = thr >= (1ull << 32); a.thr_lo = (uint32_t)std::min<uint64_t>(thr, 0xFFFFFFFFull);
+  a.random_input = random_input; a.N = N; a.seq_base = seq_base; a.seq_stride = seq_stride;
+  a.pitch = pitch; a.q0 = q0; a.count = count; a.r = d_r;
+  const unsigned grid = (unsigned)((count + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(gen_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
+  HIP_CHECK(hipGetLastError());
+  return CVD_OK;
+}
+
+int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
+                             int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream) {
+  if (M.kind != 0 || !M.d_rec) { set_error("table path needs a dense (enumerated) model"); return CVD_E_UNSUPPORTED; }
+  if (nseq <= 0) return CVD_OK;
+  TabArgs a;
+  const int R = 1 << M.dec.n;
+  a.rec = M.d_rec; a.logp1 = M.d_logp1; a.ltref = M.d_ltref; a.n = M.dec.n;
+  a.S = M.S; a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
+  const size_t lds = (size_t)M.S * R * (sizeof(double) + sizeof(uint32_t)) + (R + 1) * sizeof(double);
+  const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
+  if (lds <= 64 * 1024) {
+    hipLaunchKernelGGL(detect_table_kernel<true>, dim3(grid), dim3(kBlock), lds, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL(detect_table_kernel<false>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
+  }
+  HIP_CHECK(hipGetLastError());
+  return CVD_OK;
+}
+
+int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
+                                int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
+                                void* stream) {
+  ExpKernel kern = pick_explicit(M.dec.m, M.dec.k, M.dec.n);
+  if (!kern || !M.d_fp) { set_error("explicit path: unsupported code shape (m,k,n)"); return CVD_E_UNSUPPORTED; }
+  if (nseq <= 0) return CVD_OK;
+  ExpArgs a;
+  a.fp = M.d_fp; a.hrec = M.d_hrec; a.ltref = M.d_ltref; a.bmp = M.d_bmp;
+  a.hmask = (uint32_t)(M.hcap - 1); a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
+  a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
+  a.trace = d_trace;
+  const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
+  HIP_CHECK(hipGetLastError());
+  return CVD_OK;
+}
+
+int cvd::upload_model(cvd_model& M, int device) {
+  if (M.device == device) return CVD_OK;
+  if (M.device >= 0) free_model_device(M);
+  HIP_CHECK(hipSetDevice(device));
+  int rc;
+  if ((rc = dev_copy(M.d_ltref, M.ltref))) return rc;
+  if (M.kind == 0) {
+    if ((rc = dev_copy(M.d_rec, M.rec))) return rc;
+    if ((rc = dev_copy(M.d_logp1, M.logp1))) return rc;
+  }
+  if (M.hcap > 0) {
+    if ((rc = dev_copy(M.d_fp, M.h_fp))) return rc;
+    if ((rc = dev_copy(M.d_hrec, M.h_rec))) return rc;
+    if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
+  }
+  M.device = device;
+  return CVD_OK;
+}
+
+void cvd::free_model_device(cvd_model& M) {
+  if (M.device < 0) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(M.device);
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_fp, M.d_hrec, M.d_bmp};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
+  M.d_fp = nullptr; M.d_hrec = nullptr; M.d_bmp = nullptr;
+  M.device = -1;
+  (void)hipSetDevice(cur);
+}
+
+// ───────────────────────────── ABI: device work ─────────────────────────────
+
+namespace {
+int parse_code_dev(const cvd_code* c, CodeDesc& d) {
+  if (!c || !c->taps || c->k < 1 || c->k > kMaxK || c->n < 1 || c->n > kMaxN || c->m < 1 || c->m > kMaxM) {
+    set_error("bad code description");
+    return CVD_E_INVALID;
+  }
+  d.k = c->k; d.n = c->n; d.m = c->m;
+  for (int i = 0; i < kMaxN * kMaxK; ++i) d.gmask[i] = 0;
+  const int L = c->m + 1;
+  for (int j = 0; j < c->n; ++j)
+    for (int i = 0; i < c->k; ++i) {
+      uint32_t g = 0;
+      for (int t = 0; t < L; ++t) {
+        const uint8_t b = c->taps[(j * c->k + i) * L + t];
+        if (b > 1) { set_error("taps must be 0/1"); return CVD_E_INVALID; }
+        g |= (uint32_t)b << t;
+      }
+      d.gmask[j * c->k + i] = g;
+    }
+  return CVD_OK;
+}
+}  // namespace
+
+extern "C" int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int64_t N,
+                            int32_t random_input, int64_t seq_base, int64_t seq_stride,
+                            uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream) {
+  CodeDesc d;
+  int rc = parse_code_dev(enc, d);
+  if (rc) return rc;
+  if (!(p >= 0.0 && p <= 1.0)) { set_error("p must lie in [0, 1]"); return CVD_E_INVALID; }
+  if (N < 0 || count < 0 || q0 < 0 || q0 + count > pitch || (!d_r && N > 0 && count > 0)) {
+    set_error("bad buffer geometry");
+    return CVD_E_INVALID;
+  }
+  return launch_generate(d, (uint32_t)seed, (uint32_t)(seed >> 32), tag, noise_threshold(p), N,
+                         random_input, seq_base, seq_stride, d_r, pitch, q0, count, stream);
+}
+
+extern "C" int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
+                          int64_t n_h1, double* d_sums, int64_t* d_counts, int32_t path, void* stream) {
+  if (!model || (!d_r && N > 0 && nseq > 0) || !d_counts || N < 0 || nseq < 0 || n_h1 < 0 || n_h1 > nseq) {
+    set_error("bad detect arguments");
+    return CVD_E_INVALID;
+  }
+  int rc = check_device(*model);
+  if (rc) return rc;
+  if (path == CVD_PATH_AUTO) path = model->kind == 0 ? CVD_PATH_TABLE : CVD_PATH_EXPLICIT;
+  if (path == CVD_PATH_TABLE) return launch_detect_table(*model, d_r, N, nseq, n_h1, d_sums, d_counts, stream);
+  if (path == CVD_PATH_EXPLICIT)
+    return launch_detect_explicit(*model, d_r, N, nseq, n_h1, d_sums, d_counts, nullptr, stream);
+  set_error("unknown path");
+  return CVD_E_INVALID;
+}
+
+extern "C" int cvd_trace(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
+                         uint8_t* d_D, void* stream) {
+  if (!model || (!d_r && N > 0 && nseq > 0) || (!d_D && nseq > 0) || N < 0 || nseq < 0) {
+    set_error("bad trace arguments");
+    return CVD_E_INVALID;
+  }
+  int rc = check_device(*model);
+  if (rc) return rc;
+  // the counts of a trace launch are discarded into a scratch pair
+  int64_t* d_tmp = nullptr;
+  HIP_CHECK(hipMallocAsync((void**)&d_tmp, 2 * sizeof(int64_t), (hipStream_t)stream));
+  HIP_CHECK(hipMemsetAsync(d_tmp, 0, 2 * sizeof(int64_t), (hipStream_t)stream));
+  rc = launch_detect_explicit(*model, d_r, N, nseq, 0, nullptr, d_tmp, d_D, stream);
+  (void)hipFreeAsync(d_tmp, (hipStream_t)stream);
+  return rc;
+}
+
+extern "C" int64_t cvd_mc_workspace_bytes(const cvd_code* enc1, int64_t N, int64_t batch) {
+  if (!enc1 || enc1->n < 1 || N < 0 || batch < 0) return -1;
+  const int64_t spw = 32 / enc1->n;
+  return ((N + spw - 1) / spw) * 2 * batch * (int64_t)sizeof(uint32_t);
+}
+
+extern "C" int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2,
+                          double p, int64_t N, uint64_t seed, int64_t trial_begin, int64_t trial_end,
+                          int64_t batch, void* d_work, int64_t* d_counts, int32_t path, void* stream) {
+  if (!model || !d_work || !d_counts || trial_end < trial_begin || batch <= 0 || N < 0) {
+    set_error("bad mc_run arguments");
+    return CVD_E_INVALID;
+  }
+  CodeDesc e1, e2;
+  int rc;
+  if ((rc = parse_code_dev(enc1, e1)) || (rc = parse_code_dev(enc2, e2))) return rc;
+  if (e1.n != model->dec.n || e2.n != model->dec.n || e1.k != model->dec.k || e2.k != model->dec.k) {
+    set_error("encoder and decoder must share (k, n)");
+    return CVD_E_INVALID;
+  }
+  if (!(p >= 0.0 && p <= 1.0)) { set_error("p must lie in [0, 1]"); return CVD_E_INVALID; }
+  const uint32_t tag = grid_tag(N, p);
+  const uint64_t thr = noise_threshold(p);
+  uint32_t* r = static_cast<uint32_t*>(d_work);
+  for (int64_t b = trial_begin; b < trial_end; b += batch) {
+    const int64_t T = std::min(batch, trial_end - b);
+    if ((rc = launch_generate(e1, (uint32_t)seed, (uint32_t)(seed >> 32), tag, thr, N, 1, 2 * b, 2, r,
+                              2 * T, 0, T, stream)))
+      return rc;
+    if ((rc = launch_generate(e2, (uint32_t)seed, (uint32_t)(seed >> 32), tag, thr, N, 1, 2 * b + 1, 2, r,
+                              2 * T, T, T, stream)))
+      return rc;
+    if ((rc = cvd_detect(model, r, N, 2 * T, T, nullptr, d_counts, path, stream))) return rc;
+  }
+  return CVD_OK;
+}

@@ -1,0 +1,357 @@
+"""Host driver of the MI355X detector, mirroring the reference's call surface.
+
+Reference (So-bonkers/Detecting-Convolutional-Codes-Via-Markovian-Statistics):
+  Pd_plotter.run_experiment(k, n, m, gen1, gen2, num_iter, p_vec, learn_len,
+                            learn_burn, laplace, seed) -> DataFrame[N, p, Pd, Pc]
+                                                                    (Pd_plotter.py:176-235)
+  Pd_plotter.learn_P1_empirical(...)                               (Pd_plotter.py:123-169)
+  viterbi_markov.enumerate_markov_states_allzero / build_trellis /
+  viterbi_metric_step / branch_output_and_next_state               (viterbi_markov.py:82-195)
+  viterbi_markov.simulate_markov_sequence (missing; spec SURVEY.md §8 A5)
+
+The trial loop (Pd_plotter.py:198-233) runs on the GPU through libcvd.so:
+cvd_generate (encoder + BSC into bit-packed HBM streams) and cvd_detect
+(Eq. 4-5 recursion + log-likelihood sums + decisions + counts).  There is no
+CPU fallback: without a GPU or without libcvd.so the calls raise.
+"""
+import ctypes
+import itertools
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from .codes import Code, as_code
+
+# Pd_plotter.py:67-83
+DEFAULTS = {
+    "num_iter": 10000,
+    "p_vec": [0.001, 0.01, 0.1, 0.2, 0.3, 0.4, 0.5],
+    "seed": 12345,
+    "learn_len": None,
+    "learn_burn": 200,
+    "laplace": 1.0,
+    "save_dir": "results_experiments",
+}
+N_SPECTRUM_BY_M = {1: [5, 10, 20, 50, 100, 200], 2: [500], 3: [500], 4: [50, 100, 200, 300, 500]}
+
+# Non-enumerable codes (m = 6: > 2e8 metric states) learn on a chain of this
+# length when learn_len is None; the reference's max(5000, 200*S) needs S.
+DEFAULT_ENUM_CAP = 500_000
+DEFAULT_SPARSE_LEARN_LEN = 1_000_000
+
+
+LEARN_TAG = 0xC0DE1EA7   # CVD_LEARN_TAG: stream tag of the P̂1 learning chain
+
+
+def grid_tag(N, p):
+    """Stream tag of an (N, p) grid point (cvd_grid_tag)."""
+    return int(_lib.lib().cvd_grid_tag(int(N), float(p)))
+
+
+def _require_gpu(device):
+    if not torch.cuda.is_available():
+        raise RuntimeError("the detector runs on the GPU (HIP); no GPU is visible")
+    return torch.device("cuda", torch.cuda.current_device() if device is None else device)
+
+
+def _stream_ptr(stream=None):
+    s = torch.cuda.current_stream() if stream is None else stream
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Model:
+    """Decoder trellis (G1) + learned P̂1 + T_ref(1/2) tables (a cvd_model)."""
+
+    def __init__(self, dec, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345,
+                 enum_cap=DEFAULT_ENUM_CAP, default_learn_len=DEFAULT_SPARSE_LEARN_LEN):
+        self.dec = dec
+        self.p = float(p)
+        prm = _lib.cvd_learn_params(float(p), -1 if learn_len is None else int(learn_len),
+                                    int(learn_burn), float(laplace), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                    int(enum_cap), int(default_learn_len))
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().cvd_model_create(dec.c, ctypes.byref(prm), ctypes.byref(h)))
+        self._h = h
+        self._lib = _lib.lib()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self):
+        inf = _lib.cvd_model_info()
+        _lib.check(self._lib.cvd_model_info_get(self._h, ctypes.byref(inf)))
+        return {f: getattr(inf, f) for f, _ in inf._fields_}
+
+    def dense_P1(self):
+        S = self.info()["S"]
+        P = np.zeros((S, S), np.float64)
+        _lib.check(self._lib.cvd_model_dense_P1(self._h, P.ctypes.data, S))
+        return P
+
+    def rows(self):
+        inf = self.info()
+        R, M = 1 << inf["n"], 1 << inf["m"]
+        lp = np.zeros((inf["n_rows"], R), np.float64)
+        keys = np.zeros((inf["n_rows"], M), np.uint8)
+        _lib.check(self._lib.cvd_model_rows(self._h, lp.ctypes.data, keys.ctypes.data, inf["n_rows"]))
+        return lp, keys
+
+    def upload(self, device):
+        _lib.check(self._lib.cvd_model_upload(self._h, int(device)))
+        return self
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and h.value:
+            try:
+                self._lib.cvd_model_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+
+class Detector:
+    """One decoder (G1) on one GPU; caches learned models per (p, learning args)
+    like the reference's @lru_cache(maxsize=128) (Pd_plotter.py:123)."""
+
+    def __init__(self, k, n, m, gen1, device=None, enum_cap=DEFAULT_ENUM_CAP,
+                 default_learn_len=DEFAULT_SPARSE_LEARN_LEN):
+        self.k, self.n, self.m = int(k), int(n), int(m)
+        self.dec = as_code(gen1, m, k, n)
+        self.device = _require_gpu(device)
+        self.enum_cap = enum_cap
+        self.default_learn_len = default_learn_len
+        self._models = OrderedDict()
+
+    def model(self, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345):
+        key = (float(p), learn_len, int(learn_burn), float(laplace), int(seed))
+        if key in self._models:
+            self._models.move_to_end(key)
+            return self._models[key]
+        mod = Model(self.dec, p, learn_len, learn_burn, laplace, seed, self.enum_cap,
+                    self.default_learn_len).upload(self.device.index)
+        self._models[key] = mod
+        while len(self._models) > 128:
+            self._models.popitem(last=False)
+        return mod
+
+    def words_per_seq(self, N):
+        spw = 32 // self.n
+        return (int(N) + spw - 1) // spw
+
+    def generate(self, enc, N, p, seed, tag, seq_base, seq_stride, count, out=None, q0=0, pitch=None,
+                 random_input=True, stream=None):
+        """Received words (int32 view of uint32) [words, pitch] for `count` sequences."""
+        enc = as_code(enc, self.m, self.k, self.n)
+        pitch = count if pitch is None else pitch
+        if out is None:
+            out = torch.empty((self.words_per_seq(N), pitch), dtype=torch.int32, device=self.device)
+        _lib.check(_lib.lib().cvd_generate(enc.c, int(seed) & 0xFFFFFFFFFFFFFFFF, int(tag), float(p),
+                                           int(N), int(bool(random_input)), int(seq_base),
+                                           int(seq_stride), ctypes.c_void_p(out.data_ptr()), int(pitch),
+                                           int(q0), int(count), _stream_ptr(stream)))
+        return out
+
+    def detect(self, model, r, N, nseq, n_h1, sums=None, counts=None, path=_lib.PATH_AUTO, stream=None):
+        if counts is None:
+            counts = torch.zeros(2, dtype=torch.int64, device=self.device)
+        _lib.check(_lib.lib().cvd_detect(model.handle, ctypes.c_void_p(r.data_ptr()), int(N), int(nseq),
+                                         int(n_h1),
+                                         ctypes.c_void_p(sums.data_ptr() if sums is not None else 0),
+                                         ctypes.c_void_p(counts.data_ptr()), int(path),
+                                         _stream_ptr(stream)))
+        return counts
+
+    def trace(self, model, r, N, nseq, stream=None):
+        """D_0..D_N of every sequence on the explicit path: uint8 [N+1, nseq, 2^m]."""
+        D = torch.empty((int(N) + 1, int(nseq), 1 << self.m), dtype=torch.uint8, device=self.device)
+        _lib.check(_lib.lib().cvd_trace(model.handle, ctypes.c_void_p(r.data_ptr()), int(N), int(nseq),
+                                        ctypes.c_void_p(D.data_ptr()), _stream_ptr(stream)))
+        return D
+
+    def default_batch(self, N, trial_count, budget_bytes=4 << 30):
+        per_trial = 2 * self.words_per_seq(N) * 4
+        return int(max(1, min(trial_count, max(1024, budget_bytes // max(per_trial, 1)))))
+
+    def run_trials(self, model, gen1, gen2, N, p, seed, trial_begin, trial_end, batch=None,
+                   path=_lib.PATH_AUTO, return_sums=False, counts=None, stream=None):
+        """Global trials [trial_begin, trial_end) of one (N, p) grid point
+        (Pd_plotter.py:198-223).  Returns {"counts": (s1, s2), "sums": [T, 4]?}
+        with sums per trial = (logp1, logp1_ref, logp2, logp2_ref)."""
+        g1 = as_code(gen1, self.m, self.k, self.n)
+        g2 = as_code(gen2, self.m, self.k, self.n)
+        T = int(trial_end) - int(trial_begin)
+        if counts is None:
+            counts = torch.zeros(2, dtype=torch.int64, device=self.device)
+        if T <= 0:
+            return {"counts": counts, "sums": np.zeros((0, 4))} if return_sums else {"counts": counts}
+        batch = self.default_batch(N, T) if batch is None else int(batch)
+        lib = _lib.lib()
+        if not return_sums:
+            wsz = lib.cvd_mc_workspace_bytes(g1.c, int(N), batch)
+            work = torch.empty(max(wsz, 4) // 4, dtype=torch.int32, device=self.device)
+            _lib.check(lib.cvd_mc_run(model.handle, g1.c, g2.c, float(p), int(N),
+                                      int(seed) & 0xFFFFFFFFFFFFFFFF, int(trial_begin), int(trial_end),
+                                      batch, ctypes.c_void_p(work.data_ptr()),
+                                      ctypes.c_void_p(counts.data_ptr()), int(path), _stream_ptr(stream)))
+            return {"counts": counts}
+        tag = grid_tag(N, p)
+        out = []
+        for b in range(int(trial_begin), int(trial_end), batch):
+            Tb = min(batch, int(trial_end) - b)
+            r = torch.empty((self.words_per_seq(N), 2 * Tb), dtype=torch.int32, device=self.device)
+            self.generate(g1, N, p, seed, tag, 2 * b, 2, Tb, out=r, q0=0, pitch=2 * Tb, stream=stream)
+            self.generate(g2, N, p, seed, tag, 2 * b + 1, 2, Tb, out=r, q0=Tb, pitch=2 * Tb, stream=stream)
+            sums = torch.empty((2 * Tb, 2), dtype=torch.float64, device=self.device)
+            self.detect(model, r, N, 2 * Tb, Tb, sums=sums, counts=counts, path=path, stream=stream)
+            s = sums.cpu().numpy()
+            out.append(np.concatenate([s[:Tb], s[Tb:]], axis=1))
+        return {"counts": counts, "sums": np.concatenate(out, axis=0)}
+
+
+# ───────────────────── reference-mirroring functions ────────────────────────
+
+_DETECTORS = {}
+
+
+def _detector(k, n, m, gen1, device=None):
+    code = as_code(gen1, m, k, n)
+    key = (code.key, device)
+    if key not in _DETECTORS:
+        _DETECTORS[key] = Detector(k, n, m, code, device=device)
+    return _DETECTORS[key]
+
+
+def run_experiment(k, n, m, gen1, gen2, num_iter, p_vec, learn_len, learn_burn, laplace, seed,
+                   N_list=None, device=None, batch=None, path=_lib.PATH_AUTO, dist=None):
+    """Drop-in for Pd_plotter.run_experiment (Pd_plotter.py:176-235).
+
+    Extra keyword arguments: N_list (defaults to the reference's
+    N_SPECTRUM_BY_M.get(m, [50, 100, 200]), Pd_plotter.py:196), device, batch,
+    path, dist (a torch.distributed default group is used automatically when
+    initialised: trials are sharded by global trial id over ranks and the
+    success counts reduced with ONE all_reduce (RCCL on ROCm)).
+    """
+    import pandas as pd
+    import torch.distributed as tdist
+
+    det = _detector(k, n, m, gen1, device)
+    N_spectrum = list(N_SPECTRUM_BY_M.get(m, [50, 100, 200]) if N_list is None else N_list)
+    use_dist = dist if dist is not None else (tdist.is_available() and tdist.is_initialized())
+    rank, world = (tdist.get_rank(), tdist.get_world_size()) if use_dist else (0, 1)
+    counts = torch.zeros((len(N_spectrum), len(p_vec), 2), dtype=torch.int64, device=det.device)
+    for iN, N in enumerate(N_spectrum):
+        for ip, p in enumerate(p_vec):
+            model = det.model(p, learn_len, learn_burn, laplace, seed)
+            lo = num_iter * rank // world
+            hi = num_iter * (rank + 1) // world
+            det.run_trials(model, gen1, gen2, N, p, seed, lo, hi, batch=batch, path=path,
+                           counts=counts[iN, ip])
+    if use_dist and world > 1:
+        tdist.all_reduce(counts, op=tdist.ReduceOp.SUM)
+    c = counts.cpu().numpy()
+    rows = []
+    for iN, N in enumerate(N_spectrum):
+        for ip, p in enumerate(p_vec):
+            s1, s2 = int(c[iN, ip, 0]), int(c[iN, ip, 1])
+            rows.append({"N": N, "p": p, "Pd": s1 / num_iter, "Pc": (s1 + s2) / (2 * num_iter)})
+    return pd.DataFrame(rows)
+
+
+def learn_P1_empirical(gens_tuple, k, n, m, p, learn_len, learn_burn, laplace, seed):
+    """Mirror of Pd_plotter.py:123-169 for enumerable codes: (states, state_index, P)."""
+    gen = [[list(x) for x in row] for row in gens_tuple]
+    mod = Model(Code(gen, m, k, n), p, learn_len, learn_burn, laplace, seed)
+    if mod.info()["kind"] != 0:
+        raise _lib.CvdError("learn_P1_empirical: code is not enumerable; use Detector.model()")
+    _, keys = mod.rows()
+    states = [tuple(int(v) for v in row) for row in keys]
+    return states, {s: i for i, s in enumerate(states)}, mod.dense_P1()
+
+
+def enumerate_markov_states_allzero(generator_matrix, m, k, n, cap=DEFAULT_ENUM_CAP):
+    """Mirror of viterbi_markov.py:166-195 (native BFS): (states, transitions, all_r)."""
+    code = as_code(generator_matrix, m, k, n)
+    lib = _lib.lib()
+    S = ctypes.c_int64()
+    _lib.check(lib.cvd_enumerate(code.c, int(cap), ctypes.byref(S), None, None))
+    M, R = 1 << m, 1 << n
+    st = np.zeros((S.value, M), np.uint8)
+    nx = np.zeros((S.value, R), np.int32)
+    _lib.check(lib.cvd_enumerate(code.c, int(cap), ctypes.byref(S), st.ctypes.data, nx.ctypes.data))
+    all_r = list(itertools.product([0, 1], repeat=n))
+    states = [tuple(int(v) for v in row) for row in st]
+    transitions = {}
+    for i in range(S.value):
+        d = {}
+        for ri, r in enumerate(all_r):
+            rint = sum(b << j for j, b in enumerate(r))
+            d.setdefault(int(nx[i, rint]), []).append(r)
+        transitions[i] = d
+    return states, transitions, all_r
+
+
+class Trellis(dict):
+    """build_trellis result (viterbi_markov.py:118-132) that also carries the code."""
+
+    def __init__(self, code):
+        super().__init__()
+        self.code = code
+        out, nxt = code.tables()
+        for ns in range(1 << code.m):
+            self[ns] = []
+        for s in range(1 << code.m):
+            for U in range(1 << code.k):
+                u = tuple((U >> i) & 1 for i in range(code.k))
+                o = tuple((int(out[s, U]) >> j) & 1 for j in range(code.n))
+                self[int(nxt[s, U])].append((s, u, o))
+
+
+def build_trellis(generator_matrix, m, k, n=None):
+    n = len(generator_matrix) if n is None else n
+    return Trellis(as_code(generator_matrix, m, k, n))
+
+
+def branch_output_and_next_state(state_int, input_bits, generator_matrix, m, k):
+    code = as_code(generator_matrix, m, k, len(generator_matrix))
+    out, nxt = code.tables()
+    U = sum(int(b) << i for i, b in enumerate(input_bits))
+    o = int(out[state_int, U])
+    return tuple((o >> j) & 1 for j in range(code.n)), int(nxt[state_int, U])
+
+
+def viterbi_metric_step(D_prev, trellis, y_t):
+    """Mirror of viterbi_markov.py:139-159 (native host step)."""
+    code = trellis.code
+    D = np.asarray(D_prev, dtype=np.uint8)
+    out = np.zeros(1 << code.m, np.uint8)
+    r = sum(int(b) << j for j, b in enumerate(y_t))
+    _lib.check(_lib.lib().cvd_metric_step(code.c, D.ctypes.data, r, out.ctypes.data))
+    return tuple(int(v) for v in out)
+
+
+def simulate_markov_sequence(generator_matrix, m, k, n, N, p_val, random_input=True, seed=None,
+                             decoder=None, tag=LEARN_TAG, seq_id=0, device=None):
+    """The reference's missing simulator (called at Pd_plotter.py:149-155, 212, 219),
+    on the GPU: encoder -> BSC(p) (cvd_generate) -> D_0..D_N on trellis(decoder)
+    (cvd_trace).  Returns {"metrics": [tuple, ...], "received": np.ndarray}."""
+    dec = as_code(decoder if decoder is not None else generator_matrix, m, k, n)
+    det = _detector(k, n, m, dec, device)
+    model = det.model(0.0, learn_len=0, learn_burn=0, laplace=1.0, seed=0)
+    sd = 0 if seed is None else int(seed)
+    r = det.generate(generator_matrix, N, p_val, sd, tag, seq_id, 1, 1, random_input=random_input)
+    D = det.trace(model, r, N, 1)[:, 0, :].cpu().numpy()
+    spw = 32 // n
+    words = r[:, 0].cpu().numpy().astype(np.uint32)
+    t = np.arange(N)
+    recv = (words[t // spw] >> ((t % spw) * n).astype(np.uint32)) & ((1 << n) - 1)
+    return {"metrics": [tuple(int(v) for v in row) for row in D], "received": recv.astype(np.int64)}
+
+
+def log_likelihood_ratio(sums):
+    """Λ_N = log P̂1(D_0^N) - log T_ref(D_0^N) per sequence (Pd_plotter.py:38)."""
+    return sums[..., 0] - sums[..., 1]
+

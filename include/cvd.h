@@ -1,0 +1,144 @@
+/*
+ * cvd.h — C-ABI of the MI355X-native Monte-Carlo relative-Viterbi-metric
+ * detector (libcvd.so).  Drop-in boundary for the reference's hot path:
+ *
+ *   reference (So-bonkers/Detecting-Convolutional-Codes-Via-Markovian-Statistics)   this ABI
+ *   ───────────────────────────────────────────────────────────────────────────   ─────────────────────
+ *   viterbi_markov.py:82-106  branch_output_and_next_state                         cvd_code_tables
+ *   viterbi_markov.py:139-159 viterbi_metric_step (Eq. 4-5)                        cvd_metric_step (host), cvd_trace (GPU)
+ *   viterbi_markov.py:166-195 enumerate_markov_states_allzero (BFS)                cvd_enumerate
+ *   viterbi_markov.py:202-230 + Pd_plotter.py:89-99  T(p) at p = 1/2              cvd_model_* (|Y(i,j)|/2^n, exact)
+ *   Pd_plotter.py:123-169     learn_P1_empirical                                   cvd_model_create
+ *   viterbi_markov.simulate_markov_sequence (MISSING; called Pd_plotter.py:149,212,219)
+ *                                                                                  cvd_generate (+ cvd_trace)
+ *   Pd_plotter.py:106-116     log_prob_sequence                                    cvd_detect (per-sequence sums)
+ *   Pd_plotter.py:198-233     trial loop, decision, Pd/Pc counting                 cvd_detect (counts) / cvd_mc_run
+ *   (none: the reference is single-process)                                        counts reduced by the caller over RCCL
+ *
+ * Conventions:
+ *   - every function returns 0 on success, a negative CVD_E* code on error;
+ *     cvd_last_error() returns a thread-local message; no C++ exception crosses the ABI;
+ *   - buffers are caller-owned; pointers named d_* are device pointers (HIP),
+ *     `stream` is a hipStream_t (NULL = default stream); launches are async;
+ *   - host tables are copied in at cvd_model_create / cvd_model_upload;
+ *   - generator taps use the reference layout taps[j][i][d] (output j, input i,
+ *     delay d = 0..m; d = 0 multiplies the current input bit), flattened row-major.
+ */
+#ifndef CVD_H
+#define CVD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CVD_ABI_VERSION 1
+
+#define CVD_OK 0
+#define CVD_E_INVALID -1      /* bad argument */
+#define CVD_E_UNSUPPORTED -2  /* code shape not supported by the requested path */
+#define CVD_E_CAPACITY -3     /* enumeration cap hit / table too large */
+#define CVD_E_HIP -4          /* HIP runtime error */
+#define CVD_E_STATE -5        /* state not in the model's index (reference: KeyError) */
+
+typedef struct cvd_code {
+  int32_t k, n, m;         /* inputs, outputs, memory */
+  const uint8_t* taps;     /* [n][k][m+1] delay-ordered taps */
+} cvd_code;
+
+typedef struct cvd_learn_params {
+  double p;                /* BSC crossover of the learning chain */
+  int64_t learn_len;       /* < 0: None -> max(5000, 200*S) (Pd_plotter.py:143-146);
+                              non-enumerable codes: default_learn_len */
+  int64_t learn_burn;      /* Pd_plotter.py:72 default 200 */
+  double laplace;          /* Pd_plotter.py:73 default 1.0 */
+  uint64_t seed;           /* learning-chain seed (Pd_plotter.py:70 default 12345) */
+  int64_t enum_cap;        /* BFS cap; above it the model is sparse (learned states only) */
+  int64_t default_learn_len; /* learn length for non-enumerable codes when learn_len < 0 */
+} cvd_learn_params;
+
+typedef struct cvd_model_info {
+  int32_t kind;            /* 0 = dense (BFS-enumerated, reference-exact), 1 = sparse (learned states) */
+  int32_t k, n, m;
+  int64_t S;               /* states in the Laplace denominator (BFS count, or learned count) */
+  int64_t n_rows;          /* rows held in the device table */
+  int64_t learn_len_eff;   /* learning chain length actually used */
+  int64_t hash_capacity;   /* explicit-path hash slots (0 if none) */
+  int32_t max_probe;       /* longest probe sequence in the hash */
+  int32_t device;          /* device holding the tables, -1 if not uploaded */
+  double logp1_unseen;     /* log P̂1 of a row never visited (sparse models) */
+} cvd_model_info;
+
+typedef struct cvd_model cvd_model;
+
+/* ---- version / errors ---------------------------------------------------- */
+int cvd_version(void);
+const char* cvd_last_error(void);
+
+/* Stream tag of the (N, p) grid point (the trial streams' Philox counter word 3). */
+#define CVD_LEARN_TAG 0xC0DE1EA7u
+uint32_t cvd_grid_tag(int64_t N, double p);
+
+/* ---- host-side code algebra (no GPU needed) --------------------------------
+ * out_sym[s*2^k + U] = output word (bit j = output j), next_state[s*2^k + U];
+ * U = sum_i u_i << i.                                  (viterbi_markov.py:82-106) */
+int cvd_code_tables(const cvd_code* code, int32_t* out_sym, int32_t* next_state);
+
+/* One Eq. 4-5 step on the host, D as 2^m bytes.          (viterbi_markov.py:139-159) */
+int cvd_metric_step(const cvd_code* dec, const uint8_t* D_prev, int32_t r, uint8_t* D_out);
+
+/* BFS over relative-metric states from D_0 = 0 (viterbi_markov.py:166-195).
+ * Writes S; if states_out != NULL it receives [min(S,cap)][2^m] bytes in discovery
+ * order; if next_out != NULL, next_out[i*2^n + r] = index of the successor.
+ * Returns CVD_E_CAPACITY if more than `cap` states exist. */
+int cvd_enumerate(const cvd_code* dec, int64_t cap, int64_t* S_out,
+                  uint8_t* states_out, int32_t* next_out);
+
+/* ---- model: decoder trellis + learned P̂1 + T_ref(1/2) ------------------------ */
+int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm, cvd_model** out);
+int cvd_model_info_get(const cvd_model* model, cvd_model_info* info);
+/* Dense models: the S x S P̂1 matrix exactly as Pd_plotter.py:166-167 builds it. */
+int cvd_model_dense_P1(const cvd_model* model, double* P_out, int64_t S);
+/* Per-row tables (host copies): logP1[row*2^n + r]; keys[row][2^m] metric bytes. */
+int cvd_model_rows(const cvd_model* model, double* logp1_out, uint8_t* keys_out, int64_t n_rows);
+int cvd_model_upload(cvd_model* model, int device);
+void cvd_model_destroy(cvd_model* model);
+
+/* ---- device work ---------------------------------------------------------- */
+/* Encoder (enc) -> BSC(p) received words for sequences q0..q0+count-1 of an
+ * interleaved buffer (r[w*pitch + q]); sequence q uses
+ * seq_id = seq_base + (q - q0) * seq_stride.  Spec of the missing
+ * simulate_markov_sequence.  d_r holds ceil(N / floor(32/n)) * pitch words. */
+int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int64_t N,
+                 int32_t random_input, int64_t seq_base, int64_t seq_stride,
+                 uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream);
+
+#define CVD_PATH_AUTO 0
+#define CVD_PATH_TABLE 1     /* enumerated state automaton (dense models) */
+#define CVD_PATH_EXPLICIT 2  /* explicit 2^m metric vector + hashed P̂1 rows */
+
+/* Detector over sequences 0..nseq-1 (pitch = nseq): per sequence the sequential
+ * fp64 sums log P̂1(D_0^N) and log T_ref(D_0^N) (Pd_plotter.py:106-116); sequences
+ * q < n_h1 are H1 streams (success iff logp1 > logref), the rest H2 streams
+ * (success iff logp1 <= logref) (Pd_plotter.py:215-223).  d_counts[0] += H1
+ * successes, d_counts[1] += H2 successes (int64, accumulated, not cleared).
+ * d_sums (nullable): [nseq][2] doubles. */
+int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
+               int64_t n_h1, double* d_sums, int64_t* d_counts, int32_t path, void* stream);
+
+/* Metric trace on the explicit path: d_D[(t*nseq + q)*2^m + s] = D_t(s), t = 0..N. */
+int cvd_trace(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
+              uint8_t* d_D, void* stream);
+
+/* One (N, p) grid point over global trials [trial_begin, trial_end): generates
+ * H1 (enc1) and H2 (enc2) streams in batches of `batch` trials into the caller's
+ * workspace d_work (cvd_mc_workspace_bytes) and accumulates d_counts[2]. */
+int64_t cvd_mc_workspace_bytes(const cvd_code* enc1, int64_t N, int64_t batch);
+int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2,
+               double p, int64_t N, uint64_t seed, int64_t trial_begin, int64_t trial_end,
+               int64_t batch, void* d_work, int64_t* d_counts, int32_t path, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CVD_H */
