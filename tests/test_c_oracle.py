@@ -1,0 +1,83 @@
+"""Pin the C oracle (oracle/cvd_oracle.c) to the Python restatement and the
+reference's golden vectors; check the product's native sparse (m = 6) model
+against the C oracle's independent restatement of the same policy.  CPU only."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import code_of
+from oracle import c_oracle as C
+from oracle import philox
+from oracle import restatement as R
+
+
+@pytest.mark.parametrize("name,N,p", [("m2_75", 500, 0.05), ("r23_m4", 301, 0.2), ("m6_133_171", 777, 0.01)])
+def test_c_stream_matches_spec(golden, name, N, p):
+    z, meta = golden
+    k, n, m, taps = code_of(meta, name)
+    tag = philox.grid_tag(N, p)
+    assert C.lib().oc_grid_tag(N, p) == tag
+    for sid in (0, 5, 2**33 + 7):
+        np.testing.assert_array_equal(C.stream(C.Code(taps, m, k, n), N, p, 77, tag, sid),
+                                      R.received_stream(taps, m, k, n, N, p, 77, tag, sid))
+
+
+@pytest.mark.parametrize("ename", ["exp_m2_75_57", "exp_m3_demo"])
+def test_c_oracle_sums_vs_reference(golden, ename):
+    z, meta = golden
+    e = meta[ename]
+    k, n, m, t1 = code_of(meta, e["g1"])
+    t2 = code_of(meta, e["g2"])[3]
+    c1, c2 = C.Code(t1, m, k, n), C.Code(t2, m, k, n)
+    iters = e["num_iter"]
+    sums = z[f"{ename}/sums"]
+    for N in e["N_list"]:
+        for ip, p in enumerate(e["p_vec"]):
+            mod = C.Model(c1, p, None, e["learn_burn"], e["laplace"], e["seed"])
+            assert mod.kind == 0
+            counts, got = mod.run_trials(c1, c2, N, p, e["seed"], 0, iters, sums=True, nthreads=4)
+            assert np.array_equal(got, sums[ip * iters:(ip + 1) * iters])
+            row = e["rows"][ip]
+            assert counts[0] / iters == row["Pd"] and (counts[0] + counts[1]) / (2 * iters) == row["Pc"]
+
+
+def test_native_sparse_model_equals_c_oracle(pkg):
+    """Product host learning (libcvd) == C oracle for the m = 6 sparse policy."""
+    cc = pkg.CONFIG_CODES["m6"]
+    for p in (0.01, 0.1):
+        mod = pkg.Model(pkg.Code(cc["gen1"], 6, 1, 2), p, 50000, 200, 1.0, 12345, enum_cap=1000)
+        lp, keys = mod.rows()
+        om = C.Model(C.Code(cc["gen1"], 6, 1, 2), p, 50000, 200, 1.0, 12345, enum_cap=1000)
+        olp, okeys = om.rows()
+        assert om.kind == 1 and mod.info()["kind"] == 1
+        np.testing.assert_array_equal(keys, okeys)
+        assert np.array_equal(lp, olp)
+        assert mod.info()["logp1_unseen"] == math.log(1.0 / om.S)
+
+
+def test_c_oracle_sparse_sums_vs_python(pkg):
+    """C oracle m = 6 sums == Python recursion over the same rows (T_ref by
+    comparing all 2^n successors)."""
+    cc = pkg.CONFIG_CODES["m6"]
+    c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
+    p, N = 0.05, 150
+    om = C.Model(c1, p, 20000, 200, 1.0, 3, enum_cap=1000)
+    counts, sums = om.run_trials(c1, c2, N, p, 3, 10, 14, sums=True, nthreads=2)
+    lp_tab, keys = om.rows()
+    index = {bytes(row): i for i, row in enumerate(keys)}
+    out, nxt = R.encoder_tables(cc["gen1"], 6, 1, 2)
+    tag = philox.grid_tag(N, p)
+    for t in range(10, 14):
+        for hyp, g in ((0, cc["gen1"]), (1, cc["gen2"])):
+            r = R.received_stream(g, 6, 1, 2, N, p, 3, tag, 2 * t + hyp)
+            D = np.zeros(64, np.int64)
+            lp = lr = 0.0
+            for rv in r:
+                i = index.get(bytes(D.astype(np.uint8)))
+                succ = [R.metric_step_vec(D, out, nxt, q, 2) for q in range(4)]
+                c = sum(np.array_equal(succ[q], succ[rv]) for q in range(4))
+                lp += lp_tab[i, rv] if i is not None else math.log(1.0 / om.S)
+                lr += math.log(c / 4)
+                D = succ[rv]
+            assert sums[t - 10, 2 * hyp] == lp and sums[t - 10, 2 * hyp + 1] == lr

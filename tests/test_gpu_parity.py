@@ -1,0 +1,241 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the
+reference's golden vectors.  Integer work (received streams, metric vectors,
+counts) is bit-exact; the fp64 log-likelihood sums are bit-exact as well,
+because both sides add the same log values in the same t order."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import code_of
+from oracle import philox
+from oracle import restatement as R
+
+pytestmark = pytest.mark.gpu
+
+
+def pack_words(r_list, n):
+    """[nseq] arrays of received words -> interleaved uint32 words [W, nseq] as int32."""
+    spw = 32 // n
+    N = len(r_list[0])
+    W = (N + spw - 1) // spw
+    out = np.zeros((W, len(r_list)), np.uint64)
+    for q, r in enumerate(r_list):
+        for t, v in enumerate(r):
+            out[t // spw, q] |= np.uint64(int(v) << (n * (t % spw)))
+    return torch.from_numpy(out.astype(np.uint32).view(np.int32)).cuda()
+
+
+def unpack_words(words, n, N):
+    w = words.cpu().numpy().view(np.uint32).astype(np.int64)
+    spw = 32 // n
+    t = np.arange(N)
+    return (w[t // spw, :] >> ((t % spw) * n)[:, None]) & ((1 << n) - 1)   # [N, nseq]
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda", 0)
+
+
+# ───────────────────────────── generator ────────────────────────────────────
+
+@pytest.mark.parametrize("name,N,p,ri", [("m2_75", 1000, 0.05, True), ("m2_75", 37, 0.5, True),
+                                          ("m3_demo", 333, 0.2, True), ("r23_m4", 1001, 0.1, True),
+                                          ("r23_m4", 23, 0.0, True), ("m6_133_171", 517, 0.03, True),
+                                          ("m6_133_171", 64, 1.0, False), ("m2_57", 1, 0.3, True)])
+def test_generator_bit_exact(pkg, golden, dev, name, N, p, ri):
+    z, meta = golden
+    k, n, m, taps = code_of(meta, name)
+    det = pkg.Detector(k, n, m, taps, device=0)
+    seed, tag, base, stride, count = 0x1234_5678_9ABC, philox.grid_tag(N, p), 7, 3, 130
+    r = det.generate(taps, N, p, seed, tag, base, stride, count, random_input=ri)
+    got = unpack_words(r, n, N)
+    for q in range(0, count, 11):
+        want = R.received_stream(taps, m, k, n, N, p, seed, tag, base + q * stride, random_input=ri)
+        np.testing.assert_array_equal(got[:, q], want)
+
+
+# ───────────────────────────── metric trace ─────────────────────────────────
+
+@pytest.mark.parametrize("name", ["m2_75", "m3_demo", "r23_m4", "m6_133_171"])
+def test_trace_vs_reference_golden(pkg, golden, dev, name):
+    """D_0..D_N of the explicit kernel == the reference's viterbi_metric_step."""
+    z, meta = golden
+    k, n, m, taps = code_of(meta, name)
+    r = z[f"{name}/trace_r"]
+    D = z[f"{name}/trace_D"]
+    det = pkg.Detector(k, n, m, taps, device=0)
+    model = det.model(0.05, learn_len=0, learn_burn=0, laplace=1.0, seed=0)
+    N = len(r)
+    # three copies, the middle one shifted by a random stream, to exercise lanes
+    rng = np.random.default_rng(5)
+    r2 = rng.integers(0, 1 << n, size=N)
+    words = pack_words([r, r2, r], n)
+    T = det.trace(model, words, N, 3).cpu().numpy()
+    np.testing.assert_array_equal(T[:, 0, :], D)
+    np.testing.assert_array_equal(T[:, 2, :], D)
+    want2 = np.array(R.metrics_from_stream(taps, m, k, n, r2[:300]), np.uint8)
+    np.testing.assert_array_equal(T[:301, 1, :], want2)
+
+
+def test_simulate_markov_sequence_spec(pkg, golden, dev):
+    z, meta = golden
+    k, n, m, taps = code_of(meta, "m3_demo")
+    g1 = code_of(meta, "m3_demo2")[3]
+    sim = pkg.simulate_markov_sequence(g1, m, k, n, 400, 0.1, True, seed=99, decoder=taps)
+    want = R.simulate_markov_sequence(g1, m, k, n, 400, 0.1, True, seed=99, decoder=taps)
+    assert sim["metrics"] == want["metrics"]
+    np.testing.assert_array_equal(sim["received"], want["received"])
+
+
+# ───────────────────── detector vs reference run_experiment ────────────────
+
+@pytest.mark.parametrize("ename", ["exp_m2_75_57", "exp_m2_75_65", "exp_m3_demo"])
+@pytest.mark.parametrize("path", [1, 2])
+def test_trial_sums_bit_exact_vs_reference(pkg, golden, dev, ename, path):
+    """Every per-trial (logp1, logp1_ref, logp2, logp2_ref) equals the value the
+    reference's own run_experiment produced (table AND explicit path)."""
+    z, meta = golden
+    e = meta[ename]
+    k, n, m, t1 = code_of(meta, e["g1"])
+    t2 = code_of(meta, e["g2"])[3]
+    det = pkg.Detector(k, n, m, t1, device=0)
+    sums = z[f"{ename}/sums"]
+    iters = e["num_iter"]
+    for N in e["N_list"]:
+        for ip, p in enumerate(e["p_vec"]):
+            model = det.model(p, None, e["learn_burn"], e["laplace"], e["seed"])
+            res = det.run_trials(model, t1, t2, N, p, e["seed"], 0, iters, batch=77, path=path,
+                                 return_sums=True)
+            assert np.array_equal(res["sums"], sums[ip * iters:(ip + 1) * iters])
+            s1 = int(np.sum(sums[ip * iters:(ip + 1) * iters, 0] > sums[ip * iters:(ip + 1) * iters, 1]))
+            s2 = int(np.sum(sums[ip * iters:(ip + 1) * iters, 2] <= sums[ip * iters:(ip + 1) * iters, 3]))
+            assert tuple(res["counts"].cpu().tolist()) == (s1, s2)
+
+
+@pytest.mark.parametrize("ename", ["exp_m2_75_57", "exp_m3_demo"])
+def test_run_experiment_dataframe(pkg, golden, dev, ename):
+    z, meta = golden
+    e = meta[ename]
+    k, n, m, t1 = code_of(meta, e["g1"])
+    t2 = code_of(meta, e["g2"])[3]
+    df = pkg.run_experiment(k, n, m, t1, t2, e["num_iter"], e["p_vec"], None, e["learn_burn"],
+                            e["laplace"], e["seed"])
+    assert df.to_dict(orient="records") == e["rows"]
+
+
+def test_mc_run_counts_batch_and_shard_invariant(pkg, dev):
+    cc = pkg.CONFIG_CODES["m2"]
+    det = pkg.Detector(1, 2, 2, cc["gen1"], device=0)
+    model = det.model(0.08, None, 200, 1.0, 5)
+    ref = det.run_trials(model, cc["gen1"], cc["gen2"], 300, 0.08, 5, 0, 5000, return_sums=True)
+    want = tuple(ref["counts"].cpu().tolist())
+    for batch in (5000, 999, 64):
+        got = det.run_trials(model, cc["gen1"], cc["gen2"], 300, 0.08, 5, 0, 5000, batch=batch)
+        assert tuple(got["counts"].cpu().tolist()) == want
+    c = torch.zeros(2, dtype=torch.int64, device=dev)
+    for lo, hi in [(0, 1234), (1234, 1235), (1235, 5000)]:
+        det.run_trials(model, cc["gen1"], cc["gen2"], 300, 0.08, 5, lo, hi, counts=c)
+    assert tuple(c.cpu().tolist()) == want
+
+
+def test_edge_cases(pkg, dev):
+    cc = pkg.CONFIG_CODES["m2"]
+    det = pkg.Detector(1, 2, 2, cc["gen1"], device=0)
+    model = det.model(0.1, None, 200, 1.0, 1)
+    # N = 0: empty metric sequences, log-likelihoods 0.0 == 0.0 -> H1 fails, H2 succeeds
+    res = det.run_trials(model, cc["gen1"], cc["gen2"], 0, 0.1, 1, 0, 10, return_sums=True)
+    assert tuple(res["counts"].cpu().tolist()) == (0, 10)
+    # empty trial range
+    res = det.run_trials(model, cc["gen1"], cc["gen2"], 50, 0.1, 1, 3, 3)
+    assert tuple(res["counts"].cpu().tolist()) == (0, 0)
+    # ragged sizes (not a multiple of the 256-lane block) and p = 0 / 1
+    for p in (0.0, 1.0):
+        mod = det.model(p, None, 200, 1.0, 1)
+        a = det.run_trials(mod, cc["gen1"], cc["gen2"], 77, p, 1, 0, 301, return_sums=True)
+        states, transitions, all_r = R.enumerate_markov_states_allzero(cc["gen1"], 2, 1, 2)
+        Tref = R.T_half(states, transitions, all_r)
+        _, sidx, P1 = R.learn_P1_empirical(cc["gen1"], 1, 2, 2, p, None, 200, 1.0, 1, states, transitions)
+        _, _, want = R.run_trials(cc["gen1"], cc["gen2"], 1, 2, 2, 77, p, 1, 290, 301, sidx, P1, Tref,
+                                  return_sums=True)
+        assert np.array_equal(a["sums"][290:], np.array(want).reshape(-1, 4))
+
+
+def test_explicit_path_equals_table_path_rate23(pkg, golden, dev):
+    z, meta = golden
+    k, n, m, t1 = code_of(meta, "r23_m4")
+    t2 = code_of(meta, "r23_m4_b")[3]
+    det = pkg.Detector(k, n, m, t1, device=0)
+    model = det.model(0.05, None, 200, 1.0, 123)
+    a = det.run_trials(model, t1, t2, 2000, 0.05, 123, 0, 700, path=1, return_sums=True)
+    b = det.run_trials(model, t1, t2, 2000, 0.05, 123, 0, 700, path=2, return_sums=True)
+    assert np.array_equal(a["sums"], b["sums"])
+    # and the first trials against the oracle
+    states, transitions, all_r = R.enumerate_markov_states_allzero(t1, m, k, n)
+    Tref = R.T_half(states, transitions, all_r)
+    _, sidx, P1 = R.learn_P1_empirical(t1, k, n, m, 0.05, None, 200, 1.0, 123, states, transitions)
+    _, _, want = R.run_trials(t1, t2, k, n, m, 2000, 0.05, 123, 0, 3, sidx, P1, Tref, return_sums=True)
+    assert np.array_equal(a["sums"][:3], np.array(want).reshape(-1, 4))
+
+
+# ─────────────────────────── m = 6 sparse model ─────────────────────────────
+
+def oracle_sums_sparse(model_rows, taps, m, k, n, r_stream, lp_unseen):
+    """Oracle recursion for a sparse model: row lookup by metric vector, unseen
+    rows -> log(1/S); T_ref count from all 2^n successors."""
+    lp_tab, keys = model_rows
+    index = {bytes(row): i for i, row in enumerate(keys)}
+    out, nxt = R.encoder_tables(taps, m, k, n)
+    D = np.zeros(1 << m, np.int64)
+    lp = lr = 0.0
+    for rv in r_stream:
+        i = index.get(bytes(D.astype(np.uint8)))
+        succ = [R.metric_step_vec(D, out, nxt, q, n) for q in range(1 << n)]
+        c = sum(np.array_equal(succ[q], succ[rv]) for q in range(1 << n))
+        lp += lp_tab[i, rv] if i is not None else lp_unseen
+        lr += math.log(max(c / (1 << n), 1e-300))
+        D = succ[rv]
+    return lp, lr
+
+
+@pytest.mark.parametrize("p", [0.02, 0.15])
+def test_m6_sparse_sums_vs_oracle(pkg, dev, p):
+    cc = pkg.CONFIG_CODES["m6"]
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    model = det.model(p, 30000, 200, 1.0, 12345)
+    inf = model.info()
+    assert inf["kind"] == 1
+    N = 400
+    res = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, 12345, 0, 200, return_sums=True)
+    rows = model.rows()
+    tag = philox.grid_tag(N, p)
+    for t in (0, 1, 57, 199):
+        for hyp, g in ((0, cc["gen1"]), (1, cc["gen2"])):
+            r = R.received_stream(g, 6, 1, 2, N, p, 12345, tag, 2 * t + hyp)
+            lp, lr = oracle_sums_sparse(rows, cc["gen1"], 6, 1, 2, r, inf["logp1_unseen"])
+            assert res["sums"][t, 2 * hyp] == lp and res["sums"][t, 2 * hyp + 1] == lr
+
+
+def test_m6_full_size_properties(pkg, dev):
+    """BASELINE size N = 1e5: counts independent of batching and sharding; the
+    trace of one full-length sequence matches the host step at sampled t."""
+    cc = pkg.CONFIG_CODES["m6"]
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    model = det.model(0.01, 200000, 200, 1.0, 12345)
+    N, T = 100000, 512
+    a = det.run_trials(model, cc["gen1"], cc["gen2"], N, 0.01, 12345, 0, T, batch=T)
+    b = torch.zeros(2, dtype=torch.int64, device=dev)
+    det.run_trials(model, cc["gen1"], cc["gen2"], N, 0.01, 12345, 0, 200, batch=100, counts=b)
+    det.run_trials(model, cc["gen1"], cc["gen2"], N, 0.01, 12345, 200, T, batch=157, counts=b)
+    assert a["counts"].cpu().tolist() == b.cpu().tolist()
+    words = det.generate(cc["gen1"], N, 0.01, 12345, 17, 0, 1, 1)
+    D = det.trace(model, words, N, 1)[:, 0, :].cpu().numpy()
+    r = unpack_words(words, 2, N)[:, 0]
+    tr = pkg.build_trellis(cc["gen1"], 6, 1)
+    for t in range(0, N, 997):
+        y = ((int(r[t]) >> 0) & 1, (int(r[t]) >> 1) & 1)
+        assert pkg.viterbi_metric_step(tuple(D[t]), tr, y) == tuple(int(v) for v in D[t + 1])
+    assert D.max() <= 12
