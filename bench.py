@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Benchmark: Monte-Carlo trials/s of the relative-Viterbi-metric detector.
+
+BASELINE.json metric: "MC trials/sec at N=1e5, rate-1/2 m=6 pair, 1/2/4/8 GPUs;
+Pd match vs CPU".  Workload (configs[2]): the m = 6 pair (133,171) vs (171,133),
+N = 1e5, p swept over {0.01, 0.02, 0.05, 0.10, 0.15, 0.20}.
+
+One trial = one H1 plus one H2 sequence of length N (one iteration of
+Pd_plotter.py:210-223).  One step = one batch of `--batch` trials per GPU at
+one p of the sweep (step s uses p_grid[s % 6]): the generator kernel writes the
+batch's BSC-noised received streams to HBM (encoder + Philox noise, two
+launches: H1 with G1, H2 with G2), then the detector kernel reads them
+(Eq. 4-5 recursion for all 2^n received words, T_ref count, hashed P̂1 row
+lookup, fp64 log-likelihood sums, decisions, counts).  Both kernels are inside
+the timed region; learning P̂1 (host setup, once per p) is not.
+
+Multi-GPU (torchrun): one process per GPU, rank r takes its own global trial
+ids every step (weak scaling); the success counts are reduced with one RCCL
+all_reduce at the end of the timed region.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+from __graft_entry__ import load_package  # noqa: E402
+
+METRIC = "MC trials/sec at N=1e5, rate-1/2 m=6 pair, 1/2/4/8 GPUs; Pd match vs CPU"
+P_GRID = [0.01, 0.02, 0.05, 0.10, 0.15, 0.20]
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="m6", choices=["m6", "m2", "r23_m4"])
+    ap.add_argument("--N", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None, help="trials per GPU per step")
+    ap.add_argument("--learn-len", type=int, default=1_000_000,
+                    help="P̂1 learning chain length for non-enumerable codes")
+    ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle port (rank 0, N=1)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--pmc-traffic", default=None,
+                    help="JSON with {'detector_fetch_bytes_per_launch': ...} from a rocprofv3 --pmc pass")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    pkg = load_package()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cc = pkg.CONFIG_CODES[a.config]
+    k, n, m = cc["k"], cc["n"], cc["m"]
+    N = a.N if a.N is not None else {"m6": 100_000, "m2": 10_000, "r23_m4": 100_000}[a.config]
+    p_grid = P_GRID if a.config != "m2" else [0.05]
+    det = pkg.Detector(k, n, m, cc["gen1"], device=local)
+    g1 = pkg.Code(cc["gen1"], m, k, n)
+    g2 = pkg.Code(cc["gen2"], m, k, n)
+    models = {p: det.model(p, a.learn_len if m == 6 else None, 200, 1.0, a.seed) for p in p_grid}
+    info = models[p_grid[0]].info()
+    B = a.batch or {"m6": 196_608, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
+    W = det.words_per_seq(N)
+    r = torch.empty((W, 2 * B), dtype=torch.int32, device=det.device)
+    counts = torch.zeros((len(p_grid), 2), dtype=torch.int64, device=det.device)
+    stream = torch.cuda.current_stream()
+
+    def step(s, ev=None):
+        p = p_grid[s % len(p_grid)]
+        tb = (s * world + rank) * B            # global trial ids of this rank's batch
+        tag = pkg.grid_tag(N, p)
+        if ev is not None:
+            ev[0].record(stream)
+        det.generate(g1, N, p, a.seed, tag, 2 * tb, 2, B, out=r, q0=0, pitch=2 * B)
+        det.generate(g2, N, p, a.seed, tag, 2 * tb + 1, 2, B, out=r, q0=B, pitch=2 * B)
+        if ev is not None:
+            ev[1].record(stream)
+        det.detect(models[p], r, N, 2 * B, B, counts=counts[s % len(p_grid)])
+        if ev is not None:
+            ev[2].record(stream)
+
+    for s in range(a.warmup):
+        step(10_000 + s)
+    counts.zero_()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        step(s, events[s])
+    if dist:
+        dist.all_reduce(counts)                # the one collective: success counts over RCCL
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=det.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    gen_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    det_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    trials = a.steps * B * world
+    value = trials / elapsed
+    # roofline of the dominant kernel (detector): algorithmic bytes = the packed
+    # received streams read once, 2 * ceil(N * n / 8) bytes per trial
+    alg_bytes = B * 2 * ((N * n + 7) // 8)
+    achieved = alg_bytes / (det_ms * 1e-3) / 1e9
+    traffic = None
+    if a.pmc_traffic and os.path.exists(a.pmc_traffic):
+        with open(a.pmc_traffic) as f:
+            traffic = json.load(f).get("detector_fetch_bytes_per_launch")
+    c = counts.cpu().numpy()
+    per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, (a.steps // len(p_grid) + (i < a.steps % len(p_grid))) * B * world),
+                      "h1_successes": int(c[i, 0]), "h2_successes": int(c[i, 1])}
+             for i, p in enumerate(p_grid)}
+    out = {
+        "metric": METRIC if a.config == "m6" else f"MC trials/sec ({a.config}, N={N})",
+        "value": value,
+        "unit": "trials/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16x2 (metrics) + f64 (log-likelihood sums)",
+        "data": "synthetic: Philox4x32-10 encoder inputs and BSC(p) flips (build spec), learned P̂1",
+        "config": {"workload": f"{a.config} pair {cc['gen1']} vs {cc['gen2']}, N={N}, p-sweep {p_grid}, "
+                               f"one p per step", "N": N, "p_grid": p_grid,
+                   "trials_per_step_per_gpu": B, "model": info["kind"] and "sparse(learned)" or "dense",
+                   "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
+                   "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": f"detect_explicit_kernel<{m},{k},{n}>" if m == 6 else "detect kernel",
+                     "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms},
+        "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
+                       "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
+                       "per_p": per_p},
+    }
+    if a.cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cc, k, n, m, N, seed, learn_len, seconds):
+    """The oracle's C port of the reference path (oracle/cvd_oracle.c), OpenMP over
+    trials on this host's cores, on a bounded sample of the same workload."""
+    from oracle import c_oracle as C
+    threads = min(16, os.cpu_count() or 1)
+    c1, c2 = C.Code(cc["gen1"], m, k, n), C.Code(cc["gen2"], m, k, n)
+    p = 0.05
+    mod = C.Model(c1, p, learn_len if m == 6 else None, 200, 1.0, seed)
+    # calibrate with one trial per thread, then size the sample to ~`seconds`
+    t0 = time.perf_counter()
+    mod.run_trials(c1, c2, N, p, seed, 0, threads, nthreads=threads)
+    dt = time.perf_counter() - t0
+    ntr = max(threads, int(threads * seconds / max(dt, 1e-6)) // threads * threads)
+    t0 = time.perf_counter()
+    mod.run_trials(c1, c2, N, p, seed, threads, threads + ntr, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": ntr / dt, "unit": "trials/s", "cores": threads, "kind": "port",
+            "sample": f"{ntr} trials (H1+H2, N={N}) at p={p}, C oracle (oracle/cvd_oracle.c), "
+                      f"{threads} OpenMP threads, {dt:.1f} s",
+            "seconds": dt}
+
+
+if __name__ == "__main__":
+    main()

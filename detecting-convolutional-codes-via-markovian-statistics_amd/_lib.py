@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
 ABI_VERSION = 1
 
-PATH_AUTO, PATH_TABLE, PATH_EXPLICIT = 0, 1, 2
+PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC = 0, 1, 2, 3
 
 
 class CvdError(RuntimeError):

@@ -363,7 +363,7 @@ namespace {
 void build_hash(cvd_model& Mo) {
   const int m = Mo.dec.m, M = 1 << m, R = 1 << Mo.dec.n, nw = nib_words(m);
   int64_t cap = 64;
-  while (cap < 2 * Mo.n_rows) cap <<= 1;
+  while (cap < 4 * Mo.n_rows) cap <<= 1;   // load factor <= 1/4: most misses end at the home slot
   Mo.hcap = cap;
   Mo.h_fp.assign((size_t)cap, 0u);
   const int kw_pad = rec_key_words(m);
@@ -386,8 +386,37 @@ void build_hash(cvd_model& Mo) {
   }
 }
 
+void build_bmk1(cvd_model& Mo, const Tabs& T) {
+  // g0 = output word of (state 0, input 1): the tap-0 column over the outputs
+  const uint32_t g0 = T.out[0 * T.K + 1];
+  if (T.k != 1 || T.n < 2 || T.n > 3 || g0 == 0) return;
+  std::vector<int> reps;
+  for (int r = 0; r < T.R; ++r)
+    if ((uint32_t)r < ((uint32_t)r ^ g0)) reps.push_back(r);
+  Mo.repmap = 0; Mo.swmap = 0;
+  for (int r = 0; r < T.R; ++r) {
+    const int rep = std::min<int>(r, r ^ (int)g0);
+    const int idx = (int)(std::find(reps.begin(), reps.end(), rep) - reps.begin());
+    Mo.repmap |= (uint32_t)idx << (4 * r);
+    Mo.swmap |= (uint32_t)(r != rep) << r;
+  }
+  const int QP = (int)reps.size() / 2;
+  Mo.bmk1.assign((size_t)QP * T.M * 2, 0u);
+  for (int qp = 0; qp < QP; ++qp)
+    for (int ns = 0; ns < T.M; ++ns)
+      for (int b = 0; b < 2; ++b) {
+        const int pred = (ns >> 1) | (b << (T.m - 1));
+        const uint32_t o = T.out[pred * T.K + (ns & 1)];
+        const uint32_t b0 = __builtin_popcount(o ^ (uint32_t)reps[2 * qp]);
+        const uint32_t b1 = __builtin_popcount(o ^ (uint32_t)reps[2 * qp + 1]);
+        Mo.bmk1[((size_t)qp * T.M + ns) * 2 + b] = b0 | (b1 << 16);
+      }
+  Mo.k1_ok = true;
+}
+
 void build_bmp(cvd_model& Mo, const Tabs& T) {
   if (!explicit_supported(T.m, T.k, T.n)) return;
+  build_bmk1(Mo, T);
   const int QP = T.R / 2;
   Mo.bmp.assign((size_t)QP * T.M * T.K, 0u);
   for (int qp = 0; qp < QP; ++qp)

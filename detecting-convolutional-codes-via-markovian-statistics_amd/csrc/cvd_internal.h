@@ -33,6 +33,11 @@ struct cvd_model {
   int32_t h_rw = 0;               // record stride in dwords: key (NW, padded to even) + 2^n doubles, 16-B multiple
   std::vector<uint32_t> h_rec;    // [hcap][h_rw]
   std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
+  // k = 1 orbit kernel: successor(r ^ g0) = successor(r) with states 2j <-> 2j+1 swapped,
+  // so only the representatives rep_0 < rep_1 < ... (r < r ^ g0) get an ACS.
+  bool k1_ok = false;
+  uint32_t repmap = 0, swmap = 0;  // rep index of r (4 bits per r), r > r ^ g0 (1 bit per r)
+  std::vector<uint32_t> bmk1;      // [reps/2][2^m][2] packed (bm(rep 2qp), bm(rep 2qp+1))
 
   // device copies
   int device = -1;
@@ -42,6 +47,7 @@ struct cvd_model {
   uint32_t* d_fp = nullptr;
   uint32_t* d_hrec = nullptr;
   uint32_t* d_bmp = nullptr;
+  uint32_t* d_bmk1 = nullptr;
 };
 
 namespace cvd {
@@ -55,17 +61,15 @@ inline int rec_words(int m, int n) { return (rec_key_words(m) + 2 * (1 << n) + 3
 void pack_nibbles(const uint8_t* D, int M, uint32_t* out);
 
 // 32-bit hash pair of a nibble-packed key; must match the device version.
+// A rotate/xor-add fold (2 full-rate VALU ops per word) and two finalising
+// multiplies; h1 picks the slot, h2 is the fingerprint.
+CVD_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 CVD_HD void key_hash(const uint32_t* w, int nw, uint32_t& h1, uint32_t& h2) {
-  uint32_t a = 0x9E3779B9u ^ (uint32_t)nw, b = 0x7F4A7C15u;
-  for (int i = 0; i < nw; ++i) {
-    a = (a ^ w[i]) * 0x85EBCA6Bu;
-    a ^= a >> 15;
-    b = (b + w[i]) * 0xC2B2AE35u;
-    b ^= b >> 13;
-  }
-  a ^= a >> 16;
-  b = (b ^ (b >> 16)) * 0x27D4EB2Fu;
-  h1 = a;
+  uint32_t h = 0x9E3779B9u ^ (uint32_t)nw;
+  for (int i = 0; i < nw; ++i) h = (h ^ w[i]) + rotl32(h, 25);
+  uint32_t a = h * 0x85EBCA6Bu;
+  h1 = a ^ (a >> 16);
+  uint32_t b = (h ^ (h >> 13)) * 0xC2B2AE35u;
   h2 = b ^ (b >> 15);
 }
 
@@ -77,7 +81,7 @@ int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int6
                         int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream);
 int launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                            int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
-                           void* stream);
+                           void* stream, bool allow_k1);
 int upload_model(cvd_model& M, int device);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);

@@ -40,6 +40,12 @@ namespace {
 constexpr int kBlock = 256;
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
+// Uniform read-only tables go through the constant address space so that
+// uniform-index loads become scalar (s_load) loads into SGPRs instead of
+// per-lane vector loads the compiler would otherwise have to wait on.
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+__device__ __forceinline__ cu32* as_const(const uint32_t* p) { return (cu32*)p; }
+
 __device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
 __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
 
@@ -184,6 +190,7 @@ struct ExpArgs {
   const uint32_t* hrec;     // [hcap][RW]
   const double* ltref;      // [R + 1]
   const uint32_t* bmp;      // [QP][M][K] packed branch metrics (bm(2qp), bm(2qp+1))
+  uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
   uint32_t hmask;
   int32_t max_probe;
   double lp_unseen;
@@ -193,6 +200,19 @@ struct ExpArgs {
   int64_t* counts;
   uint8_t* trace;
 };
+
+// pk16 minimum over L registers as a log-depth tree (independent ops issue back to back)
+template <int L>
+__device__ __forceinline__ us2 tree_min(const uint32_t (&A)[L]) {
+  us2 t[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) t[i] = as_us2(A[i]);
+#pragma unroll
+  for (int w = L / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int i = 0; i < w; ++i) t[i] = __builtin_elementwise_min(t[i], t[i + w]);
+  return t[0];
+}
 
 template <int m, int k, int n>
 struct Shape {
@@ -253,27 +273,25 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
 #pragma unroll
         for (int s = 0; s < S::M; ++s) dup[s] = ((Dw[s >> 3] >> (4 * (s & 7))) & 15u) * 0x10001u;
         uint32_t P[S::QP][S::NG];
+        cu32* bmp = as_const(a.bmp);
 #pragma unroll
         for (int qp = 0; qp < S::QP; ++qp) {
-          us2 mu = as_us2(0xFFFFFFFFu);
+          uint32_t A[S::M];
 #pragma unroll
-          for (int g = 0; g < S::NG; ++g) {
-            uint32_t packed = 0;
+          for (int ns_ = 0; ns_ < S::M; ++ns_) {
+            us2 best;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int ns_ = 4 * g + e;
-              us2 best;
-#pragma unroll
-              for (int b = 0; b < S::K; ++b) {
-                const int pred = (ns_ >> k) | (b << (m - k));
-                const us2 c = as_us2(dup[pred]) + as_us2(a.bmp[(qp * S::M + ns_) * S::K + b]);
-                best = b == 0 ? c : __builtin_elementwise_min(best, c);
-              }
-              mu = __builtin_elementwise_min(mu, best);
-              packed |= as_u32(best) << (4 * e);
+            for (int b = 0; b < S::K; ++b) {
+              const int pred = (ns_ >> k) | (b << (m - k));
+              const us2 c = as_us2(dup[pred]) + as_us2(bmp[(qp * S::M + ns_) * S::K + b]);
+              best = b == 0 ? c : __builtin_elementwise_min(best, c);
             }
-            P[qp][g] = packed;
+            A[ns_] = as_u32(best);
           }
+          const us2 mu = tree_min<S::M>(A);
+#pragma unroll
+          for (int g = 0; g < S::NG; ++g)
+            P[qp][g] = A[4 * g] | (A[4 * g + 1] << 4) | (A[4 * g + 2] << 8) | (A[4 * g + 3] << 12);
           // Eq. 5: subtract the minimum from every nibble of both halves
           const uint32_t muN = ((uint32_t)mu.x * 0x1111u) | (((uint32_t)mu.y * 0x1111u) << 16);
 #pragma unroll
@@ -338,7 +356,238 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
 
+
+// ─────────────── k = 1 orbit kernel (the m = 6 headline path) ──────────────
+//
+// For k = 1, flipping the input bit XORs the branch output with g0 (the tap-0
+// column), so the Eq. 4 successor for r ^ g0 is the successor for r with the
+// states 2j <-> 2j+1 exchanged (linearity of viterbi_markov.py:82-106).  Only
+// the representatives r < r ^ g0 (2^n / 2 words) get an add-compare-select;
+// their partners are a nibble swap.  Two representatives share one packed-16
+// instruction (lo / hi halves).
+//
+// Per lane (one sequence):
+//   Dp[i]  = (D(2i), D(2i+1)) un-normalised 16-bit pair (renormalised once per
+//            32-bit input word); a half is broadcast into the packed adds by op_sel
+//   key[]  = the normalised D_{t-1}, nibble-packed: the hash key of its P̂1 row
+// Per step: ACS -> per-rep minimum -> per group of 4 states: normalised nibble
+// pack P, its pair swap S, observed word, T_ref comparisons, next Dp pairs.
+template <int m, int n>
+__global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
+  constexpr int M = 1 << m, H = M / 2, R = 1 << n, QP = R / 4, NG = M / 4, NP = M / 2;
+  constexpr int NW = M >= 8 ? M / 8 : 1, KW = (NW + 1) & ~1, RW = (KW + 2 * R + 3) & ~3;
+  constexpr int SPW = 32 / n;
+  constexpr int CH = (H >= 4) ? 4 : H;   // butterflies per table chunk (16 words)
+  static_assert(m >= 2 && (n == 2 || n == 3), "k1 orbit kernel shape");
+  __shared__ double s_lt[R + 1];
+  if (threadIdx.x <= R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  __syncthreads();
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = q < a.nseq;
+  double lp = 0.0, lr = 0.0;
+  if (valid) {
+    uint32_t Dp[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) Dp[i] = 0u;
+    uint32_t key[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) key[w] = 0u;
+    if (a.trace) write_trace<m, 1, n>(a.trace, 0, a.nseq, q, key);
+    const int64_t nwords = (a.N + SPW - 1) / SPW;
+    int64_t t = 0;
+    for (int64_t wi = 0; wi < nwords; ++wi) {
+      uint32_t word = a.r[wi * a.nseq + q];
+      const int ns = (int)min((int64_t)SPW, a.N - wi * SPW);
+      uint32_t mu_obs = 0;
+      for (int i = 0; i < ns; ++i) {
+        const uint32_t rr = word & (uint32_t)(R - 1);
+        word >>= n;
+        const uint32_t rep = (a.repmap >> (4u * rr)) & 15u;
+        const uint32_t sw = (a.swmap >> rr) & 1u;
+        const uint32_t qr = rep >> 1, hsh = (rep & 1u) * 16u;
+
+        // (1) P̂1 row of D_{t-1}: issue the first probe now, resolve after the ACS
+        uint32_t h1, h2;
+        key_hash(key, NW, h1, h2);
+        uint32_t slot = h1 & a.hmask;
+        const uint32_t fpv = h2 | 1u;
+        const uint32_t f0 = a.fp[slot];
+        const uint32_t* rec0 = a.hrec + (size_t)slot * RW;
+        uint32_t key0[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) key0[w] = rec0[w];
+        const double l0 = reinterpret_cast<const double*>(rec0 + KW)[rr];
+
+        // (2) Eq. 4 for the representatives: A[qp][ns] = (rep 2qp, rep 2qp+1),
+        //     with the Eq. 5 minimum kept in four running accumulators.
+        // Branch metrics: 4 packed words per butterfly, read with scalar loads
+        // (constant address space -> SGPR operands of the packed adds) in
+        // chunks of CH butterflies, software-pipelined one chunk ahead.  Each
+        // chunk pointer is laundered through an asm that depends on the previous
+        // chunk's results, so neither LICM nor the scheduler can hoist the whole
+        // table into SGPRs (which spills).
+        cu32* bmbase = as_const(a.bmp);
+        constexpr int NCH = QP * H / CH;
+        uint32_t bmv[2][4 * CH];
+        uint32_t A[QP][M];
+        us2 mu[QP];
+        us2 m4[4];
+        {
+          cu32* p0 = bmbase;
+          asm volatile("" : "+s"(p0) : "v"(Dp[0]));   // per-step: not loop invariant
+#pragma unroll
+          for (int z = 0; z < 4 * CH; ++z) bmv[0][z] = p0[z];
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int qp = c / (H / CH), j0 = (c % (H / CH)) * CH;
+          if (c + 1 < NCH) {
+            // the next chunk's pointer depends on every output of the previous
+            // chunk: its scalar loads fly while this chunk computes, and no pass
+            // can pull more of the table forward (or push this chunk's ALU work
+            // past them)
+            cu32* pn = bmbase + (c + 1) * CH * 4;
+            if (c == 0) {
+              asm volatile("" : "+s"(pn) : "v"(Dp[0]));
+            } else {
+              const int cp = c - 1, qq = cp / (H / CH), jp = (cp % (H / CH)) * CH;
+              uint32_t* ap = &A[qq][2 * jp];
+              static_assert(CH == 4 || H < 4, "chunk barrier written for 4 butterflies");
+              if constexpr (CH == 4) {
+                asm volatile("" : "+s"(pn), "+v"(ap[0]), "+v"(ap[1]), "+v"(ap[2]), "+v"(ap[3]),
+                                  "+v"(ap[4]), "+v"(ap[5]), "+v"(ap[6]), "+v"(ap[7]));
+              }
+            }
+#pragma unroll
+            for (int z = 0; z < 4 * CH; ++z) bmv[(c + 1) & 1][z] = pn[z];
+          }
+          if (j0 == 0) {
+#pragma unroll
+            for (int z = 0; z < 4; ++z) m4[z] = as_us2(0xFFFFFFFFu);
+          }
+#pragma unroll
+          for (int jj = 0; jj < CH; ++jj) {       // butterfly j: preds j, j+H -> 2j, 2j+1
+            const int j = j0 + jj;
+            const uint32_t* b4 = &bmv[c & 1][4 * jj];
+            const us2 pa = as_us2(Dp[j >> 1]), pb = as_us2(Dp[(j + H) >> 1]);
+            const us2 da = (j & 1) ? __builtin_shufflevector(pa, pa, 1, 1) : __builtin_shufflevector(pa, pa, 0, 0);
+            const us2 db = ((j + H) & 1) ? __builtin_shufflevector(pb, pb, 1, 1) : __builtin_shufflevector(pb, pb, 0, 0);
+            const us2 e0 = __builtin_elementwise_min(da + as_us2(b4[0]), db + as_us2(b4[1]));
+            const us2 e1 = __builtin_elementwise_min(da + as_us2(b4[2]), db + as_us2(b4[3]));
+            A[qp][2 * j] = as_u32(e0);
+            A[qp][2 * j + 1] = as_u32(e1);
+            m4[(2 * j) & 3] = __builtin_elementwise_min(m4[(2 * j) & 3], e0);
+            m4[(2 * j + 1) & 3] = __builtin_elementwise_min(m4[(2 * j + 1) & 3], e1);
+          }
+          if (j0 + CH == H)
+            mu[qp] = __builtin_elementwise_min(__builtin_elementwise_min(m4[0], m4[1]),
+                                               __builtin_elementwise_min(m4[2], m4[3]));
+        }
+        // (3) resolve the P̂1 row of D_{t-1} (exact key compare, linear probing)
+        double lpv = a.lp_unseen;
+        {
+          bool eq = f0 == fpv;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) eq = eq && (key0[w] == key[w]);
+          if (eq) {
+            lpv = l0;
+          } else if (f0 != 0u) {
+            for (int pr = 1; pr <= a.max_probe; ++pr) {
+              slot = (slot + 1u) & a.hmask;
+              const uint32_t f = a.fp[slot];
+              if (f == 0u) break;
+              if (f == fpv) {
+                const uint32_t* rc = a.hrec + (size_t)slot * RW;
+                bool e2 = true;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) e2 = e2 && (rc[w] == key[w]);
+                if (e2) { lpv = reinterpret_cast<const double*>(rc + KW)[rr]; break; }
+              }
+            }
+          }
+        }
+        lp += lpv;            // Pd_plotter.py:115, T = P̂1
+        // (4) per group of 4 states: normalised nibble pack P (both reps), its
+        //     pair swap S (the partners r ^ g0), the observed word (-> next key),
+        //     the T_ref comparisons, and the next step's metric pairs.
+        const uint32_t bb = (rep & 1u) * 2u;
+        const uint32_t lo_sel = bb | ((bb + 1u) << 8), hi_sel = (bb + 4u) | ((bb + 5u) << 8);
+        const uint32_t psel = sw ? (hi_sel | (lo_sel << 16)) : (lo_sel | (hi_sel << 16));
+        uint32_t accP[QP], accS[QP];
+#pragma unroll
+        for (int qp = 0; qp < QP; ++qp) { accP[qp] = 0u; accS[qp] = 0u; }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          uint32_t Pg[QP], Sg[QP];
+#pragma unroll
+          for (int qp = 0; qp < QP; ++qp) {
+            const us2 mq = mu[qp];
+            const uint32_t y0 = as_u32(as_us2(A[qp][4 * g]) - mq);
+            const uint32_t y1 = as_u32(as_us2(A[qp][4 * g + 1]) - mq);
+            const uint32_t y2 = as_u32(as_us2(A[qp][4 * g + 2]) - mq);
+            const uint32_t y3 = as_u32(as_us2(A[qp][4 * g + 3]) - mq);
+            Pg[qp] = y0 | (y1 << 4) | (y2 << 8) | (y3 << 12);
+            Sg[qp] = ((Pg[qp] << 4) & 0xF0F0F0F0u) | ((Pg[qp] >> 4) & 0x0F0F0F0Fu);
+          }
+          uint32_t x = sw ? Sg[0] : Pg[0];
+#pragma unroll
+          for (int qp = 1; qp < QP; ++qp) x = (qr == (uint32_t)qp) ? (sw ? Sg[qp] : Pg[qp]) : x;
+          const uint32_t o16 = (x >> hsh) & 0xFFFFu;
+          const uint32_t od = o16 * 0x10001u;
+#pragma unroll
+          for (int qp = 0; qp < QP; ++qp) { accP[qp] |= Pg[qp] ^ od; accS[qp] |= Sg[qp] ^ od; }
+          if (NW == 1) {
+            if (g == 0) key[0] = o16; else key[0] |= o16 << 16;
+          } else {
+            if ((g & 1) == 0) key[g >> 1] = o16; else key[g >> 1] |= o16 << 16;
+          }
+#pragma unroll
+          for (int pi = 2 * g; pi < 2 * g + 2 && pi < NP; ++pi) {
+            uint32_t e0 = A[0][2 * pi], e1 = A[0][2 * pi + 1];
+#pragma unroll
+            for (int qp = 1; qp < QP; ++qp) {
+              e0 = (qr == (uint32_t)qp) ? A[qp][2 * pi] : e0;
+              e1 = (qr == (uint32_t)qp) ? A[qp][2 * pi + 1] : e1;
+            }
+            Dp[pi] = __builtin_amdgcn_perm(e1, e0, psel);   // (D_t(2pi), D_t(2pi+1))
+          }
+        }
+        uint32_t c = 0;
+#pragma unroll
+        for (int qp = 0; qp < QP; ++qp)
+          c += ((accP[qp] & 0xFFFFu) == 0u) + ((accP[qp] >> 16) == 0u) + ((accS[qp] & 0xFFFFu) == 0u) +
+               ((accS[qp] >> 16) == 0u);
+        lr += s_lt[c];        // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
+        mu_obs = (as_u32(mu[0]) >> hsh) & 0xFFFFu;
+#pragma unroll
+        for (int qp = 1; qp < QP; ++qp) mu_obs = (qr == (uint32_t)qp) ? ((as_u32(mu[qp]) >> hsh) & 0xFFFFu) : mu_obs;
+        ++t;
+        if (a.trace) write_trace<m, 1, n>(a.trace, t, a.nseq, q, key);
+      }
+      // renormalise the carried metrics once per input word (16-bit headroom)
+      const us2 mud = as_us2(mu_obs * 0x10001u);
+#pragma unroll
+      for (int pi = 0; pi < NP; ++pi) Dp[pi] = as_u32(as_us2(Dp[pi]) - mud);
+    }
+    if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+  }
+  count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
+}
+
 using ExpKernel = void (*)(ExpArgs);
+ExpKernel pick_k1(int m, int n) {
+  if (n == 2) {
+    switch (m) {
+      case 2: return detect_k1_kernel<2, 2>;
+      case 3: return detect_k1_kernel<3, 2>;
+      case 4: return detect_k1_kernel<4, 2>;
+      case 5: return detect_k1_kernel<5, 2>;
+      case 6: return detect_k1_kernel<6, 2>;
+    }
+  }
+  return nullptr;
+}
+
 ExpKernel pick_explicit(int m, int k, int n) {
   if (k == 1 && n == 2) {
     switch (m) {
@@ -409,12 +658,14 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
 
 int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                                 int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
-                                void* stream) {
-  ExpKernel kern = pick_explicit(M.dec.m, M.dec.k, M.dec.n);
+                                void* stream, bool allow_k1) {
+  ExpKernel k1 = (allow_k1 && M.k1_ok && M.d_bmk1) ? pick_k1(M.dec.m, M.dec.n) : nullptr;
+  ExpKernel kern = k1 ? k1 : pick_explicit(M.dec.m, M.dec.k, M.dec.n);
   if (!kern || !M.d_fp) { set_error("explicit path: unsupported code shape (m,k,n)"); return CVD_E_UNSUPPORTED; }
   if (nseq <= 0) return CVD_OK;
   ExpArgs a;
-  a.fp = M.d_fp; a.hrec = M.d_hrec; a.ltref = M.d_ltref; a.bmp = M.d_bmp;
+  a.fp = M.d_fp; a.hrec = M.d_hrec; a.ltref = M.d_ltref; a.bmp = k1 ? M.d_bmk1 : M.d_bmp;
+  a.repmap = M.repmap; a.swmap = M.swmap;
   a.hmask = (uint32_t)(M.hcap - 1); a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   a.trace = d_trace;
@@ -438,6 +689,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_fp, M.h_fp))) return rc;
     if ((rc = dev_copy(M.d_hrec, M.h_rec))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
+    if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
   }
   M.device = device;
   return CVD_OK;
@@ -448,11 +700,11 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_fp, M.d_hrec, M.d_bmp};
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_fp, M.d_hrec, M.d_bmp, M.d_bmk1};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
-  M.d_fp = nullptr; M.d_hrec = nullptr; M.d_bmp = nullptr;
+  M.d_fp = nullptr; M.d_hrec = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
   M.device = -1;
   (void)hipSetDevice(cur);
 }
@@ -507,8 +759,9 @@ extern "C" int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N
   if (rc) return rc;
   if (path == CVD_PATH_AUTO) path = model->kind == 0 ? CVD_PATH_TABLE : CVD_PATH_EXPLICIT;
   if (path == CVD_PATH_TABLE) return launch_detect_table(*model, d_r, N, nseq, n_h1, d_sums, d_counts, stream);
-  if (path == CVD_PATH_EXPLICIT)
-    return launch_detect_explicit(*model, d_r, N, nseq, n_h1, d_sums, d_counts, nullptr, stream);
+  if (path == CVD_PATH_EXPLICIT || path == CVD_PATH_EXPLICIT_GENERIC)
+    return launch_detect_explicit(*model, d_r, N, nseq, n_h1, d_sums, d_counts, nullptr, stream,
+                                  path == CVD_PATH_EXPLICIT);
   set_error("unknown path");
   return CVD_E_INVALID;
 }
@@ -525,7 +778,7 @@ extern "C" int cvd_trace(const cvd_model* model, const uint32_t* d_r, int64_t N,
   int64_t* d_tmp = nullptr;
   HIP_CHECK(hipMallocAsync((void**)&d_tmp, 2 * sizeof(int64_t), (hipStream_t)stream));
   HIP_CHECK(hipMemsetAsync(d_tmp, 0, 2 * sizeof(int64_t), (hipStream_t)stream));
-  rc = launch_detect_explicit(*model, d_r, N, nseq, 0, nullptr, d_tmp, d_D, stream);
+  rc = launch_detect_explicit(*model, d_r, N, nseq, 0, nullptr, d_tmp, d_D, stream, true);
   (void)hipFreeAsync(d_tmp, (hipStream_t)stream);
   return rc;
 }

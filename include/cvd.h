@@ -115,7 +115,8 @@ int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int
 
 #define CVD_PATH_AUTO 0
 #define CVD_PATH_TABLE 1     /* enumerated state automaton (dense models) */
-#define CVD_PATH_EXPLICIT 2  /* explicit 2^m metric vector + hashed P̂1 rows */
+#define CVD_PATH_EXPLICIT 2  /* explicit 2^m metric vector + hashed P̂1 rows (k=1 orbit kernel when possible) */
+#define CVD_PATH_EXPLICIT_GENERIC 3  /* explicit path, ACS for every received word (no orbit reduction) */
 
 /* Detector over sequences 0..nseq-1 (pitch = nseq): per sequence the sequential
  * fp64 sums log P̂1(D_0^N) and log T_ref(D_0^N) (Pd_plotter.py:106-116); sequences

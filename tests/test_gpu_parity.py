@@ -239,3 +239,23 @@ def test_m6_full_size_properties(pkg, dev):
         y = ((int(r[t]) >> 0) & 1, (int(r[t]) >> 1) & 1)
         assert pkg.viterbi_metric_step(tuple(D[t]), tr, y) == tuple(int(v) for v in D[t + 1])
     assert D.max() <= 12
+
+
+@pytest.mark.parametrize("name,g2name,N,p", [("m2_75", "m2_57", 700, 0.1), ("m3_demo", "m3_demo2", 900, 0.05),
+                                             ("m6_133_171", "m6_171_133", 1500, 0.05),
+                                             ("m6_133_171", "m6_171_133", 333, 0.2)])
+def test_orbit_kernel_equals_generic_explicit(pkg, golden, dev, name, g2name, N, p):
+    """k = 1 orbit kernel (ACS only for r < r ^ g0) == generic explicit kernel
+    (ACS for every received word) == table automaton (dense codes)."""
+    z, meta = golden
+    k, n, m, t1 = code_of(meta, name)
+    t2 = code_of(meta, g2name)[3]
+    det = pkg.Detector(k, n, m, t1, device=0)
+    model = det.model(p, 20000 if m == 6 else None, 200, 1.0, 77)
+    a = det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=pkg.PATH_EXPLICIT, return_sums=True)
+    b = det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=pkg.PATH_EXPLICIT_GENERIC, return_sums=True)
+    assert np.array_equal(a["sums"], b["sums"])
+    assert a["counts"].cpu().tolist() == b["counts"].cpu().tolist()
+    if m < 6:
+        c = det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=pkg.PATH_TABLE, return_sums=True)
+        assert np.array_equal(a["sums"], c["sums"])
