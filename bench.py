@@ -51,8 +51,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle port (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--pmc-traffic", default=None,
-                    help="JSON with {'detector_fetch_bytes_per_launch': ...} from a rocprofv3 --pmc pass")
+    ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "detector_pmc.json"),
+                    help="per-launch detector FETCH_SIZE summary of a rocprofv3 --pmc pass "
+                         "(profiles/collect.sh); used only when its config/batch/N match this run")
     return ap.parse_args()
 
 
@@ -78,8 +79,7 @@ def main():
     models = {p: det.model(p, a.learn_len if m == 6 else None, 200, 1.0, a.seed) for p in p_grid}
     info = models[p_grid[0]].info()
     B = a.batch or {"m6": 196_608, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
-    W = det.words_per_seq(N)
-    r = torch.empty((W, 2 * B), dtype=torch.int32, device=det.device)
+    r = det.stream_buffer(N, 2 * B)
     counts = torch.zeros((len(p_grid), 2), dtype=torch.int64, device=det.device)
     stream = torch.cuda.current_stream()
 
@@ -132,10 +132,13 @@ def main():
     # received streams read once, 2 * ceil(N * n / 8) bytes per trial
     alg_bytes = B * 2 * ((N * n + 7) // 8)
     achieved = alg_bytes / (det_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, traffic_src = None, None
     if a.pmc_traffic and os.path.exists(a.pmc_traffic):
         with open(a.pmc_traffic) as f:
-            traffic = json.load(f).get("detector_fetch_bytes_per_launch")
+            pmc = json.load(f)
+        if (pmc.get("config"), pmc.get("batch"), pmc.get("N")) == (a.config, B, N):
+            traffic = pmc.get("detector_fetch_bytes_per_launch")
+            traffic_src = os.path.relpath(a.pmc_traffic, ROOT) + " (rocprofv3 FETCH_SIZE x1024 x2, gfx950 correction)"
     c = counts.cpu().numpy()
     per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, (a.steps // len(p_grid) + (i < a.steps % len(p_grid))) * B * world),
                       "h1_successes": int(c[i, 0]), "h2_successes": int(c[i, 1])}
@@ -160,7 +163,8 @@ def main():
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": f"detect_explicit_kernel<{m},{k},{n}>" if m == 6 else "detect kernel",
+                     "kernel": "detect_k1_kernel<6,2> (k=1 orbit explicit path)" if m == 6 else "detect kernel",
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
                        "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),

@@ -49,6 +49,20 @@ __device__ __forceinline__ cu32* as_const(const uint32_t* p) { return (cu32*)p; 
 __device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
 __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
 
+// Received-word layout in HBM (include/cvd.h): words are grouped in 16-byte
+// chunks per sequence; word w of sequence q lives at
+// r[((w >> 2) * pitch + q) * 4 + (w & 3)], so each lane moves 16 B per load
+// and a wave reads / writes 1 KiB contiguously.
+__device__ __forceinline__ size_t chunk_index(int64_t w4, int64_t pitch, int64_t q) {
+  return ((size_t)w4 * (size_t)pitch + (size_t)q) * 4;
+}
+__device__ __forceinline__ uint32_t next_word(const uint32_t* r, int64_t pitch, int64_t q, int64_t w,
+                                              uint4& cache) {
+  if ((w & 3) == 0) cache = *reinterpret_cast<const uint4*>(r + chunk_index(w >> 2, pitch, q));
+  const int e = (int)(w & 3);
+  return e == 0 ? cache.x : e == 1 ? cache.y : e == 2 ? cache.z : cache.w;
+}
+
 // Wave-level success counting: one 64-bit atomic per wave and hypothesis.
 __device__ __forceinline__ void count_decisions(bool valid, bool is_h1, double lp, double lr,
                                                 int64_t* counts) {
@@ -83,7 +97,15 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
   uint32_t s = 0;
   int64_t cblk = -1;
   U4 cval{0, 0, 0, 0};
-  for (int64_t w = 0; w < nwords; ++w) {
+  uint32_t out4[4] = {0u, 0u, 0u, 0u};
+  const int64_t nw4 = (nwords + 3) & ~(int64_t)3;
+  for (int64_t w = 0; w < nw4; ++w) {
+    if (w >= nwords) {               // zero padding of the last 16-byte chunk
+      out4[w & 3] = 0u;
+      if ((w & 3) == 3)
+        *reinterpret_cast<uint4*>(a.r + chunk_index(w >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
+      continue;
+    }
     const int64_t t0 = w * spw;
     const int ns = (int)min((int64_t)spw, a.N - t0);
     // BSC flips of the word's n*ns code bits (noise uniform g = t*n + j)
@@ -124,7 +146,9 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
       word |= enc_out(a.enc, s, U) << (uint32_t)(n * i);
       s = enc_next(a.enc, s, U);
     }
-    a.r[w * a.pitch + q] = word ^ nmask;
+    out4[w & 3] = word ^ nmask;
+    if ((w & 3) == 3)
+      *reinterpret_cast<uint4*>(a.r + chunk_index(w >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
   }
 }
 
@@ -166,8 +190,9 @@ __global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
     const uint32_t rmask = (uint32_t)R - 1u;
     const int64_t nwords = (a.N + spw - 1) / spw;
     uint32_t st = 0;                     // index of D_0 = 0 (first BFS state)
+    uint4 cache;
     for (int64_t w = 0; w < nwords; ++w) {
-      uint32_t word = a.r[w * a.nseq + q];
+      uint32_t word = next_word(a.r, a.nseq, q, w, cache);
       const int ns = (int)min((int64_t)spw, a.N - w * spw);
       for (int i = 0; i < ns; ++i) {
         const uint32_t idx = st * (uint32_t)R + (word & rmask);
@@ -250,8 +275,9 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
     if (a.trace) write_trace<m, k, n>(a.trace, 0, a.nseq, q, Dw);
     const int64_t nwords = (a.N + S::SPW - 1) / S::SPW;
     int64_t t = 0;
+    uint4 cache;
     for (int64_t wi = 0; wi < nwords; ++wi) {
-      uint32_t word = a.r[wi * a.nseq + q];
+      uint32_t word = next_word(a.r, a.nseq, q, wi, cache);
       const int ns = (int)min((int64_t)S::SPW, a.N - wi * S::SPW);
       for (int i = 0; i < ns; ++i) {
         const uint32_t rr = word & (uint32_t)(S::R - 1);
@@ -395,8 +421,9 @@ __global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
     if (a.trace) write_trace<m, 1, n>(a.trace, 0, a.nseq, q, key);
     const int64_t nwords = (a.N + SPW - 1) / SPW;
     int64_t t = 0;
+    uint4 cache;
     for (int64_t wi = 0; wi < nwords; ++wi) {
-      uint32_t word = a.r[wi * a.nseq + q];
+      uint32_t word = next_word(a.r, a.nseq, q, wi, cache);
       const int ns = (int)min((int64_t)SPW, a.N - wi * SPW);
       uint32_t mu_obs = 0;
       for (int i = 0; i < ns; ++i) {
@@ -786,7 +813,8 @@ extern "C" int cvd_trace(const cvd_model* model, const uint32_t* d_r, int64_t N,
 extern "C" int64_t cvd_mc_workspace_bytes(const cvd_code* enc1, int64_t N, int64_t batch) {
   if (!enc1 || enc1->n < 1 || N < 0 || batch < 0) return -1;
   const int64_t spw = 32 / enc1->n;
-  return ((N + spw - 1) / spw) * 2 * batch * (int64_t)sizeof(uint32_t);
+  const int64_t w4 = ((N + spw - 1) / spw + 3) / 4;
+  return w4 * 4 * 2 * batch * (int64_t)sizeof(uint32_t);
 }
 
 extern "C" int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2,

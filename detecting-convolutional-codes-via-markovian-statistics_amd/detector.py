@@ -139,16 +139,21 @@ class Detector:
         return mod
 
     def words_per_seq(self, N):
+        """Received words per sequence, padded to whole 16-byte chunks."""
         spw = 32 // self.n
-        return (int(N) + spw - 1) // spw
+        return ((int(N) + spw - 1) // spw + 3) // 4 * 4
+
+    def stream_buffer(self, N, pitch):
+        """Device buffer for `pitch` sequences: [W/4, pitch, 4] words (include/cvd.h layout)."""
+        return torch.empty((self.words_per_seq(N) // 4, int(pitch), 4), dtype=torch.int32, device=self.device)
 
     def generate(self, enc, N, p, seed, tag, seq_base, seq_stride, count, out=None, q0=0, pitch=None,
                  random_input=True, stream=None):
-        """Received words (int32 view of uint32) [words, pitch] for `count` sequences."""
+        """Received words (int32 view of uint32) [W/4, pitch, 4] for `count` sequences."""
         enc = as_code(enc, self.m, self.k, self.n)
         pitch = count if pitch is None else pitch
         if out is None:
-            out = torch.empty((self.words_per_seq(N), pitch), dtype=torch.int32, device=self.device)
+            out = self.stream_buffer(N, pitch)
         _lib.check(_lib.lib().cvd_generate(enc.c, int(seed) & 0xFFFFFFFFFFFFFFFF, int(tag), float(p),
                                            int(N), int(bool(random_input)), int(seq_base),
                                            int(seq_stride), ctypes.c_void_p(out.data_ptr()), int(pitch),
@@ -202,7 +207,7 @@ class Detector:
         out = []
         for b in range(int(trial_begin), int(trial_end), batch):
             Tb = min(batch, int(trial_end) - b)
-            r = torch.empty((self.words_per_seq(N), 2 * Tb), dtype=torch.int32, device=self.device)
+            r = self.stream_buffer(N, 2 * Tb)
             self.generate(g1, N, p, seed, tag, 2 * b, 2, Tb, out=r, q0=0, pitch=2 * Tb, stream=stream)
             self.generate(g2, N, p, seed, tag, 2 * b + 1, 2, Tb, out=r, q0=Tb, pitch=2 * Tb, stream=stream)
             sums = torch.empty((2 * Tb, 2), dtype=torch.float64, device=self.device)
@@ -226,39 +231,28 @@ def _detector(k, n, m, gen1, device=None):
 
 
 def run_experiment(k, n, m, gen1, gen2, num_iter, p_vec, learn_len, learn_burn, laplace, seed,
-                   N_list=None, device=None, batch=None, path=_lib.PATH_AUTO, dist=None):
+                   N_list=None, device=None, batch=None, path=_lib.PATH_AUTO):
     """Drop-in for Pd_plotter.run_experiment (Pd_plotter.py:176-235).
 
     Extra keyword arguments: N_list (defaults to the reference's
     N_SPECTRUM_BY_M.get(m, [50, 100, 200]), Pd_plotter.py:196), device, batch,
-    path, dist (a torch.distributed default group is used automatically when
-    initialised: trials are sharded by global trial id over ranks and the
-    success counts reduced with ONE all_reduce (RCCL on ROCm)).
+    path.  When a torch.distributed default group is initialised (one process
+    per GPU), trials are sharded by global trial id over the ranks and the
+    success counts reduced with ONE all_reduce (RCCL on ROCm); every rank
+    returns the same DataFrame.
     """
     import pandas as pd
-    import torch.distributed as tdist
+    from .distributed import run_sharded, pd_rows
 
     det = _detector(k, n, m, gen1, device)
     N_spectrum = list(N_SPECTRUM_BY_M.get(m, [50, 100, 200]) if N_list is None else N_list)
-    use_dist = dist if dist is not None else (tdist.is_available() and tdist.is_initialized())
-    rank, world = (tdist.get_rank(), tdist.get_world_size()) if use_dist else (0, 1)
-    counts = torch.zeros((len(N_spectrum), len(p_vec), 2), dtype=torch.int64, device=det.device)
-    for iN, N in enumerate(N_spectrum):
-        for ip, p in enumerate(p_vec):
-            model = det.model(p, learn_len, learn_burn, laplace, seed)
-            lo = num_iter * rank // world
-            hi = num_iter * (rank + 1) // world
-            det.run_trials(model, gen1, gen2, N, p, seed, lo, hi, batch=batch, path=path,
-                           counts=counts[iN, ip])
-    if use_dist and world > 1:
-        tdist.all_reduce(counts, op=tdist.ReduceOp.SUM)
-    c = counts.cpu().numpy()
-    rows = []
-    for iN, N in enumerate(N_spectrum):
-        for ip, p in enumerate(p_vec):
-            s1, s2 = int(c[iN, ip, 0]), int(c[iN, ip, 1])
-            rows.append({"N": N, "p": p, "Pd": s1 / num_iter, "Pc": (s1 + s2) / (2 * num_iter)})
-    return pd.DataFrame(rows)
+
+    def count_fn(iN, N, ip, p, lo, hi, out):
+        model = det.model(p, learn_len, learn_burn, laplace, seed)
+        det.run_trials(model, gen1, gen2, N, p, seed, lo, hi, batch=batch, path=path, counts=out)
+
+    counts = run_sharded(count_fn, N_spectrum, list(p_vec), num_iter, det.device)
+    return pd.DataFrame(pd_rows(counts, N_spectrum, list(p_vec), num_iter))
 
 
 def learn_P1_empirical(gens_tuple, k, n, m, p, learn_len, learn_burn, laplace, seed):
@@ -345,7 +339,7 @@ def simulate_markov_sequence(generator_matrix, m, k, n, N, p_val, random_input=T
     r = det.generate(generator_matrix, N, p_val, sd, tag, seq_id, 1, 1, random_input=random_input)
     D = det.trace(model, r, N, 1)[:, 0, :].cpu().numpy()
     spw = 32 // n
-    words = r[:, 0].cpu().numpy().astype(np.uint32)
+    words = r[:, 0, :].reshape(-1).cpu().numpy().astype(np.uint32)
     t = np.arange(N)
     recv = (words[t // spw] >> ((t % spw) * n).astype(np.uint32)) & ((1 << n) - 1)
     return {"metrics": [tuple(int(v) for v in row) for row in D], "received": recv.astype(np.int64)}

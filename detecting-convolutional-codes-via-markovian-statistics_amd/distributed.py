@@ -1,0 +1,54 @@
+"""Trial sharding over ranks and the one count reduction.
+
+One process per GPU.  Every (N, p) grid point's global trial range
+[0, num_iter) is split into contiguous per-rank blocks; because the trial
+streams are keyed by the global trial id (Philox counter, see include/cvd.h),
+the per-rank success counts add up to exactly the single-GPU counts for any
+world size.  The only collective is one SUM all_reduce of the
+[n_N, n_p, 2] int64 count tensor (RCCL over xGMI for CUDA/HIP tensors, gloo on
+CPU), issued once after all grid points.
+"""
+import torch
+
+
+def shard(num_trials, rank, world):
+    """Contiguous block of global trial ids for `rank` (covers [0, num_trials) exactly)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    return num_trials * rank // world, num_trials * (rank + 1) // world
+
+
+def dist_info():
+    import torch.distributed as tdist
+    if tdist.is_available() and tdist.is_initialized():
+        return tdist.get_rank(), tdist.get_world_size()
+    return 0, 1
+
+
+def run_sharded(count_fn, N_list, p_vec, num_iter, device, rank=None, world=None):
+    """counts[iN, ip, :] += count_fn(iN, N, ip, p, lo, hi, out) for this rank's
+    trial block, then one all_reduce.  `count_fn` accumulates (s1, s2) into the
+    2-element tensor `out` (device-side for the GPU engine)."""
+    import torch.distributed as tdist
+    r0, w0 = dist_info()
+    rank = r0 if rank is None else rank
+    world = w0 if world is None else world
+    counts = torch.zeros((len(N_list), len(p_vec), 2), dtype=torch.int64, device=device)
+    lo, hi = shard(num_iter, rank, world)
+    for iN, N in enumerate(N_list):
+        for ip, p in enumerate(p_vec):
+            count_fn(iN, N, ip, p, lo, hi, counts[iN, ip])
+    if world > 1:
+        tdist.all_reduce(counts, op=tdist.ReduceOp.SUM)
+    return counts
+
+
+def pd_rows(counts, N_list, p_vec, num_iter):
+    """Rows {N, p, Pd, Pc} exactly as Pd_plotter.py:225-233."""
+    c = counts.cpu().numpy()
+    rows = []
+    for iN, N in enumerate(N_list):
+        for ip, p in enumerate(p_vec):
+            s1, s2 = int(c[iN, ip, 0]), int(c[iN, ip, 1])
+            rows.append({"N": N, "p": p, "Pd": s1 / num_iter, "Pc": (s1 + s2) / (2 * num_iter)})
+    return rows

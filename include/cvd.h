@@ -106,9 +106,12 @@ void cvd_model_destroy(cvd_model* model);
 
 /* ---- device work ---------------------------------------------------------- */
 /* Encoder (enc) -> BSC(p) received words for sequences q0..q0+count-1 of an
- * interleaved buffer (r[w*pitch + q]); sequence q uses
+ * interleaved buffer; sequence q uses
  * seq_id = seq_base + (q - q0) * seq_stride.  Spec of the missing
- * simulate_markov_sequence.  d_r holds ceil(N / floor(32/n)) * pitch words. */
+ * simulate_markov_sequence.  Layout: W = ceil(N / floor(32/n)) words per
+ * sequence, step i of a word in bits [n*i, n*i+n); words grouped in 16-byte
+ * chunks: word w of sequence q at d_r[((w/4)*pitch + q)*4 + w%4] (16-B aligned);
+ * d_r holds ceil(W/4)*4*pitch words. */
 int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int64_t N,
                  int32_t random_input, int64_t seq_base, int64_t seq_stride,
                  uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream);

@@ -16,22 +16,25 @@ pytestmark = pytest.mark.gpu
 
 
 def pack_words(r_list, n):
-    """[nseq] arrays of received words -> interleaved uint32 words [W, nseq] as int32."""
+    """[nseq] arrays of received words -> device buffer [W/4, nseq, 4] (include/cvd.h layout)."""
     spw = 32 // n
     N = len(r_list[0])
-    W = (N + spw - 1) // spw
+    W = ((N + spw - 1) // spw + 3) // 4 * 4
     out = np.zeros((W, len(r_list)), np.uint64)
     for q, r in enumerate(r_list):
         for t, v in enumerate(r):
             out[t // spw, q] |= np.uint64(int(v) << (n * (t % spw)))
-    return torch.from_numpy(out.astype(np.uint32).view(np.int32)).cuda()
+    lay = out.astype(np.uint32).reshape(W // 4, 4, len(r_list)).transpose(0, 2, 1).copy()
+    return torch.from_numpy(lay.view(np.int32)).cuda()
 
 
 def unpack_words(words, n, N):
-    w = words.cpu().numpy().view(np.uint32).astype(np.int64)
+    """device buffer [W/4, nseq, 4] -> received words [N, nseq]."""
+    b = words.cpu().numpy().view(np.uint32).astype(np.int64)
+    w = b.transpose(0, 2, 1).reshape(-1, b.shape[1])   # [W, nseq]
     spw = 32 // n
     t = np.arange(N)
-    return (w[t // spw, :] >> ((t % spw) * n)[:, None]) & ((1 << n) - 1)   # [N, nseq]
+    return (w[t // spw, :] >> ((t % spw) * n)[:, None]) & ((1 << n) - 1)
 
 
 @pytest.fixture(scope="module")
