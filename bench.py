@@ -120,7 +120,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gen_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    det_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    det_each = [e[1].elapsed_time(e[2]) for e in events]
+    det_ms = float(np.mean(det_each))
 
     if rank != 0:
         if dist:
@@ -168,6 +169,7 @@ def main():
                      "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
                        "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
+                       "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
                        "per_p": per_p},
     }
     if a.cpu_baseline and world == 1:

@@ -361,15 +361,20 @@ extern "C" int cvd_enumerate(const cvd_code* dec, int64_t cap, int64_t* S_out, u
 namespace {
 
 void build_hash(cvd_model& Mo) {
+  // Explicit-path row table: an open-addressing directory over the
+  // nibble-packed metric vectors (fingerprints + keys) and, per slot, the row
+  // record {log P̂1[r], slot of successor(r) or -1}.  The successor slots let a
+  // sequence walk learned rows without hashing (table mode).
   const int m = Mo.dec.m, M = 1 << m, R = 1 << Mo.dec.n, nw = nib_words(m);
   int64_t cap = 64;
   while (cap < 4 * Mo.n_rows) cap <<= 1;   // load factor <= 1/4: most misses end at the home slot
   Mo.hcap = cap;
   Mo.h_fp.assign((size_t)cap, 0u);
-  const int kw_pad = rec_key_words(m);
-  Mo.h_rw = rec_words(m, Mo.dec.n);
-  Mo.h_rec.assign((size_t)cap * Mo.h_rw, 0u);
+  Mo.h_key.assign((size_t)cap * nw, 0u);
+  Mo.h_rsw = row_words(Mo.dec.n);
+  Mo.h_row.assign((size_t)cap * Mo.h_rsw, 0u);
   Mo.max_probe = 0;
+  std::vector<int64_t> slot_of((size_t)Mo.n_rows);
   std::vector<uint32_t> kw((size_t)nw);
   for (int64_t i = 0; i < Mo.n_rows; ++i) {
     pack_nibbles(Mo.keys.data() + (size_t)i * M, M, kw.data());
@@ -380,10 +385,18 @@ void build_hash(cvd_model& Mo) {
     while (Mo.h_fp[slot]) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
     Mo.max_probe = std::max(Mo.max_probe, probe);
     Mo.h_fp[slot] = h2 | 1u;
-    uint32_t* rec = Mo.h_rec.data() + slot * Mo.h_rw;
-    for (int w = 0; w < nw; ++w) rec[w] = kw[w];
-    std::memcpy(rec + kw_pad, Mo.logp1.data() + (size_t)i * R, sizeof(double) * R);
+    for (int w = 0; w < nw; ++w) Mo.h_key[slot * nw + w] = kw[w];
+    slot_of[(size_t)i] = (int64_t)slot;
   }
+  for (int64_t i = 0; i < Mo.n_rows; ++i) {
+    uint32_t* rw = Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw;
+    std::memcpy(rw, Mo.logp1.data() + (size_t)i * R, sizeof(double) * R);
+    for (int r = 0; r < R; ++r) {
+      const int64_t j = Mo.row_next[(size_t)i * R + r];
+      rw[2 * R + r] = (uint32_t)(j >= 0 ? (int32_t)slot_of[(size_t)j] : -1);
+    }
+  }
+  Mo.slot0 = (int32_t)slot_of[0];   // D_0 = 0 is row 0 in both model kinds
 }
 
 void build_bmk1(cvd_model& Mo, const Tabs& T) {
@@ -488,6 +501,7 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
     Mo->rowsum.assign((size_t)S, 0.0);
     for (int64_t s = 0; s < S; ++s) {
       for (int r = 0; r < R; ++r) succ[r] = next[(size_t)s * R + r];
+      for (int r = 0; r < R; ++r) Mo->row_next.push_back(succ[r]);
       Mo->rowsum[(size_t)s] = p1_row(S, prm->laplace, memo, succ.data(), cnt.data() + (size_t)s * R, R,
                                      Mo->logp1.data() + (size_t)s * R, &nz);
       for (auto& e : nz) Mo->p1_nz.push_back({s, e.first, e.second});
@@ -541,6 +555,7 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
         step_host(T, keys.data() + (size_t)s * M, (uint32_t)r, Dn.data());
         succ[r] = map.find(Dn.data());
       }
+      for (int r = 0; r < R; ++r) Mo->row_next.push_back(succ[r]);
       p1_row(S, prm->laplace, memo, succ.data(), cnt.data() + (size_t)s * R, R,
              Mo->logp1.data() + (size_t)s * R);
     }

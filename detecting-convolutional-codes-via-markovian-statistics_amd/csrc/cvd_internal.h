@@ -29,9 +29,12 @@ struct cvd_model {
   // explicit-path hash over nibble-packed keys
   int64_t hcap = 0;               // power of two, 0 = none
   int32_t max_probe = 0;
+  std::vector<int64_t> row_next;  // [n_rows][2^n] row index of successor(row, r), -1 if not a row
   std::vector<uint32_t> h_fp;     // [hcap] fingerprint | 1, 0 = empty
-  int32_t h_rw = 0;               // record stride in dwords: key (NW, padded to even) + 2^n doubles, 16-B multiple
-  std::vector<uint32_t> h_rec;    // [hcap][h_rw]
+  std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector
+  int32_t h_rsw = 0;              // row record stride in dwords (row_words)
+  std::vector<uint32_t> h_row;    // [hcap][h_rsw]: log P̂1[r] (2^n f64), successor slot[r] (2^n i32)
+  int32_t slot0 = 0;              // slot of D_0 = 0
   std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
   // k = 1 orbit kernel: successor(r ^ g0) = successor(r) with states 2j <-> 2j+1 swapped,
   // so only the representatives rep_0 < rep_1 < ... (r < r ^ g0) get an ACS.
@@ -45,7 +48,8 @@ struct cvd_model {
   double* d_logp1 = nullptr;
   double* d_ltref = nullptr;
   uint32_t* d_fp = nullptr;
-  uint32_t* d_hrec = nullptr;
+  uint32_t* d_hkey = nullptr;
+  uint32_t* d_hrow = nullptr;
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
 };
@@ -54,8 +58,8 @@ namespace cvd {
 
 void set_error(const std::string& msg);
 inline int nib_words(int m) { return (1 << m) >= 8 ? (1 << m) / 8 : 1; }
-inline int rec_key_words(int m) { return (nib_words(m) + 1) & ~1; }   // doubles start 8-B aligned
-inline int rec_words(int m, int n) { return (rec_key_words(m) + 2 * (1 << n) + 3) & ~3; }
+// row record: 2^n doubles + 2^n int32 successor slots, padded to 16 B
+CVD_HD int row_words(int n) { return (3 * (1 << n) + 3) & ~3; }
 
 // Nibble packing of a metric vector: state s in nibble s (word s / 8, bits 4*(s % 8)).
 void pack_nibbles(const uint8_t* D, int M, uint32_t* out);

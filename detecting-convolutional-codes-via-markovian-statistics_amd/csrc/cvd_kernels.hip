@@ -211,19 +211,134 @@ __global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
 // ────────────────────────── explicit metric path ────────────────────────────
 
 struct ExpArgs {
-  const uint32_t* fp;       // [hcap]
-  const uint32_t* hrec;     // [hcap][RW]
+  const uint32_t* fp;       // [hcap] fingerprint | 1, 0 = empty
+  const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors
+  const uint32_t* hrow;     // [hcap][row_words(n)]: log P̂1[r] (f64), successor slot[r] (i32, -1 = not a row)
   const double* ltref;      // [R + 1]
-  const uint32_t* bmp;      // [QP][M][K] packed branch metrics (bm(2qp), bm(2qp+1))
+  const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
   uint32_t hmask;
   int32_t max_probe;
+  int32_t slot0;            // slot of D_0 = 0
   double lp_unseen;
   int64_t N, nseq, n_h1;
   const uint32_t* r;
   double* sums;
   int64_t* counts;
   uint8_t* trace;
+};
+
+// Received words of one sequence, one word of lookahead (the next step's r is
+// known before the current step ends, so its P̂1 row entry can be prefetched).
+template <int n>
+struct StreamReader {
+  static constexpr int SPW = 32 / n;
+  static constexpr uint32_t MASK = (1u << n) - 1u;
+  const uint32_t* r;
+  int64_t pitch, q, N, nwords, wi;
+  uint4 cache;
+  uint32_t cur, nxt;
+  int left;
+  __device__ int steps_in(int64_t w) const { return (int)min((int64_t)SPW, N - w * SPW); }
+  __device__ void init(const uint32_t* r_, int64_t pitch_, int64_t q_, int64_t N_) {
+    r = r_; pitch = pitch_; q = q_; N = N_;
+    nwords = (N + SPW - 1) / SPW;
+    cur = nxt = 0u; left = 0; wi = 0;
+    if (nwords > 0) { cur = next_word(r, pitch, q, 0, cache); left = steps_in(0); }
+    wi = 1;
+    if (wi < nwords) nxt = next_word(r, pitch, q, wi, cache);
+  }
+  __device__ uint32_t peek() const { return cur & MASK; }
+  __device__ uint32_t peek_next() const { return left > 1 ? ((cur >> n) & MASK) : (nxt & MASK); }
+  __device__ void advance() {
+    if (left > 1) { cur >>= n; --left; return; }
+    cur = nxt;
+    left = wi < nwords ? steps_in(wi) : 0;
+    ++wi;
+    if (wi < nwords) nxt = next_word(r, pitch, q, wi, cache);
+  }
+};
+
+// Lookup of the P̂1 row of the current metric state.  A learned row stores the
+// slot of its successor for every received word, so a sequence that stays in
+// learned states walks rows with one small prefetched load per step and no
+// hashing ("table mode").  After an unvisited state the successor is unknown
+// and the next state is hashed: its fingerprint is fetched one step ahead, the
+// key and row entries only on a fingerprint match (mid-step), and the exact
+// key compare happens when the step resolves.  slot: >= 0 known row,
+// -1 known unvisited row, -2 pending hash probe (hs, fpv, pf).
+template <int NW, int R>
+struct RowCursor {
+  static constexpr int RSW = (3 * R + 3) & ~3;
+  int32_t slot, pnx;
+  uint32_t hs, fpv, pf;
+  double plp;
+  uint32_t pkey[NW];
+  __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
+    const uint32_t* rw = a.hrow + (size_t)s * RSW;
+    plp = reinterpret_cast<const double*>(rw)[rn];
+    pnx = (int32_t)rw[2 * R + rn];
+  }
+  __device__ void start(const ExpArgs& a, uint32_t r0) {
+    slot = a.slot0; pf = 0u; hs = 0u; fpv = 0u;
+    prefetch_row(a, slot, r0);
+  }
+  __device__ void mid(const ExpArgs& a, uint32_t r) {
+    if (slot == -2 && pf == fpv) {
+      const uint32_t* k = a.hkey + (size_t)hs * NW;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) pkey[w] = k[w];
+      prefetch_row(a, (int32_t)hs, r);
+    }
+  }
+  // log P̂1(row(D_{t-1}), r); afterwards `slot` describes row(D_t)
+  __device__ double resolve(const ExpArgs& a, const uint32_t (&key)[NW], uint32_t r) {
+    double lpv = a.lp_unseen;
+    int32_t ns = -2;
+    if (slot >= 0) {
+      lpv = plp; ns = pnx;
+    } else if (slot == -2 && pf != 0u) {
+      bool eq = pf == fpv;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) eq = eq && (pkey[w] == key[w]);
+      if (eq) {
+        lpv = plp; ns = pnx;
+      } else {
+        uint32_t sl = hs;
+        for (int pr = 1; pr <= a.max_probe; ++pr) {
+          sl = (sl + 1u) & a.hmask;
+          const uint32_t f = a.fp[sl];
+          if (f == 0u) break;
+          if (f == fpv) {
+            const uint32_t* k = a.hkey + (size_t)sl * NW;
+            bool e2 = true;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) e2 = e2 && (k[w] == key[w]);
+            if (e2) {
+              const uint32_t* rw = a.hrow + (size_t)sl * RSW;
+              lpv = reinterpret_cast<const double*>(rw)[r];
+              ns = (int32_t)rw[2 * R + r];
+              break;
+            }
+          }
+        }
+      }
+    }
+    slot = ns;
+    return lpv;
+  }
+  // D_t's key is known: issue the next step's loads
+  __device__ void prefetch(const ExpArgs& a, const uint32_t (&key)[NW], uint32_t rn) {
+    if (slot >= 0) {
+      prefetch_row(a, slot, rn);
+    } else if (slot == -2) {
+      uint32_t h1, h2;
+      key_hash(key, NW, h1, h2);
+      hs = h1 & a.hmask;
+      fpv = h2 | 1u;
+      pf = a.fp[hs];
+    }
+  }
 };
 
 // pk16 minimum over L registers as a log-depth tree (independent ops issue back to back)
@@ -273,27 +388,15 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
 #pragma unroll
     for (int w = 0; w < S::NW; ++w) Dw[w] = 0u;
     if (a.trace) write_trace<m, k, n>(a.trace, 0, a.nseq, q, Dw);
-    const int64_t nwords = (a.N + S::SPW - 1) / S::SPW;
-    int64_t t = 0;
-    uint4 cache;
-    for (int64_t wi = 0; wi < nwords; ++wi) {
-      uint32_t word = next_word(a.r, a.nseq, q, wi, cache);
-      const int ns = (int)min((int64_t)S::SPW, a.N - wi * S::SPW);
-      for (int i = 0; i < ns; ++i) {
-        const uint32_t rr = word & (uint32_t)(S::R - 1);
-        word >>= n;
-        // (1) P̂1 row of D_{t-1}: first probe issued now, resolved after the ACS.
-        uint32_t h1, h2;
-        key_hash(Dw, S::NW, h1, h2);
-        uint32_t slot = h1 & a.hmask;
-        const uint32_t fpv = h2 | 1u;
-        const uint32_t f0 = a.fp[slot];
-        const uint32_t* rec0 = a.hrec + (size_t)slot * S::RW;
-        uint32_t key0[S::NW];
-#pragma unroll
-        for (int w = 0; w < S::NW; ++w) key0[w] = rec0[w];
-        const double l0 = reinterpret_cast<const double*>(rec0 + S::KW)[rr];
-
+    StreamReader<n> rd;
+    rd.init(a.r, a.nseq, q, a.N);
+    RowCursor<S::NW, S::R> cur;
+    cur.start(a, rd.peek());
+    for (int64_t t = 1; t <= a.N; ++t) {
+      {
+        const uint32_t rr = rd.peek();
+        const uint32_t rn = t < a.N ? rd.peek_next() : 0u;
+        cur.mid(a, rr);
         // (2) Eq. 4 for every received word q', two per packed-16 instruction.
         uint32_t dup[S::M];
 #pragma unroll
@@ -341,29 +444,8 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
           for (int g = 0; g < S::NG; ++g) acc |= P[qp][g] ^ (obs[g] * 0x10001u);
           c += ((acc & 0xFFFFu) == 0u) + ((acc >> 16) == 0u);
         }
-        // (4) resolve the P̂1 lookup (exact key compare; linear probing)
-        double lpv = a.lp_unseen;
-        {
-          bool eq = f0 == fpv;
-#pragma unroll
-          for (int w = 0; w < S::NW; ++w) eq = eq && (key0[w] == Dw[w]);
-          if (eq) {
-            lpv = l0;
-          } else if (f0 != 0u) {
-            for (int pr = 1; pr <= a.max_probe; ++pr) {
-              slot = (slot + 1u) & a.hmask;
-              const uint32_t f = a.fp[slot];
-              if (f == 0u) break;
-              if (f == fpv) {
-                const uint32_t* rc = a.hrec + (size_t)slot * S::RW;
-                bool e2 = true;
-#pragma unroll
-                for (int w = 0; w < S::NW; ++w) e2 = e2 && (rc[w] == Dw[w]);
-                if (e2) { lpv = reinterpret_cast<const double*>(rc + S::KW)[rr]; break; }
-              }
-            }
-          }
-        }
+        // (4) P̂1 row of D_{t-1}
+        const double lpv = cur.resolve(a, Dw, rr);
         lp += lpv;            // Pd_plotter.py:115 with T = P̂1
         lr += s_lt[c];        // Pd_plotter.py:115 with T = T_ref(1/2) = c / 2^n
         // (5) D_t becomes the state
@@ -373,8 +455,9 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
 #pragma unroll
           for (int w = 0; w < S::NW; ++w) Dw[w] = obs[2 * w] | (obs[2 * w + 1] << 16);
         }
-        ++t;
         if (a.trace) write_trace<m, k, n>(a.trace, t, a.nseq, q, Dw);
+        cur.prefetch(a, Dw, rn);
+        rd.advance();
       }
     }
     if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
@@ -390,21 +473,25 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
 // states 2j <-> 2j+1 exchanged (linearity of viterbi_markov.py:82-106).  Only
 // the representatives r < r ^ g0 (2^n / 2 words) get an add-compare-select;
 // their partners are a nibble swap.  Two representatives share one packed-16
-// instruction (lo / hi halves).
+// instruction (lo / hi halves).  This kernel is specialised to n = 2 (one
+// representative pair; the (133,171) headline code and every rate-1/2 k=1 code
+// with taps[0] != 0 on some output).
 //
 // Per lane (one sequence):
-//   Dp[i]  = (D(2i), D(2i+1)) un-normalised 16-bit pair (renormalised once per
-//            32-bit input word); a half is broadcast into the packed adds by op_sel
-//   key[]  = the normalised D_{t-1}, nibble-packed: the hash key of its P̂1 row
-// Per step: ACS -> per-rep minimum -> per group of 4 states: normalised nibble
-// pack P, its pair swap S, observed word, T_ref comparisons, next Dp pairs.
+//   Dp[i]  = (D(2i), D(2i+1)) normalised 16-bit pair; op_sel broadcasts one
+//            half into both halves of the packed adds for free
+//   key[]  = the normalised D_{t-1}, nibble-packed (hash key of its P̂1 row)
+// Per step, everything is produced per group of 4 states as soon as its two
+// butterflies are done, so no full 2^m vector of raw ACS outputs stays live:
+//   P_g  = raw ACS outputs (<= (ceil(m)+1)n <= 15) nibble-packed, both reps;
+//          the minimum is subtracted once per packed word afterwards
+//   Dn_i = next metric pairs of the observed representative (v_perm_b32)
 template <int m, int n>
 __global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
-  constexpr int M = 1 << m, H = M / 2, R = 1 << n, QP = R / 4, NG = M / 4, NP = M / 2;
-  constexpr int NW = M >= 8 ? M / 8 : 1, KW = (NW + 1) & ~1, RW = (KW + 2 * R + 3) & ~3;
-  constexpr int SPW = 32 / n;
-  constexpr int CH = (H >= 4) ? 4 : H;   // butterflies per table chunk (16 words)
-  static_assert(m >= 2 && (n == 2 || n == 3), "k1 orbit kernel shape");
+  constexpr int M = 1 << m, H = M / 2, R = 1 << n, NG = M / 4, NP = M / 2;
+  constexpr int NW = M >= 8 ? M / 8 : 1;
+  constexpr int CH = (H >= 4) ? 4 : H;   // butterflies per branch-metric chunk (16 words)
+  static_assert(m >= 2 && n == 2, "k1 orbit kernel shape");
   __shared__ double s_lt[R + 1];
   if (threadIdx.x <= R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
   __syncthreads();
@@ -419,182 +506,120 @@ __global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
 #pragma unroll
     for (int w = 0; w < NW; ++w) key[w] = 0u;
     if (a.trace) write_trace<m, 1, n>(a.trace, 0, a.nseq, q, key);
-    const int64_t nwords = (a.N + SPW - 1) / SPW;
-    int64_t t = 0;
-    uint4 cache;
-    for (int64_t wi = 0; wi < nwords; ++wi) {
-      uint32_t word = next_word(a.r, a.nseq, q, wi, cache);
-      const int ns = (int)min((int64_t)SPW, a.N - wi * SPW);
-      uint32_t mu_obs = 0;
-      for (int i = 0; i < ns; ++i) {
-        const uint32_t rr = word & (uint32_t)(R - 1);
-        word >>= n;
-        const uint32_t rep = (a.repmap >> (4u * rr)) & 15u;
+    cu32* bmbase = as_const(a.bmp);
+    StreamReader<n> rd;
+    rd.init(a.r, a.nseq, q, a.N);
+    RowCursor<NW, R> cur;
+    cur.start(a, rd.peek());
+    for (int64_t t = 1; t <= a.N; ++t) {
+      {
+        const uint32_t rr = rd.peek();
+        const uint32_t rn = t < a.N ? rd.peek_next() : 0u;
+        const uint32_t rep = (a.repmap >> (4u * rr)) & 15u;   // 0 or 1: lo / hi half
         const uint32_t sw = (a.swmap >> rr) & 1u;
-        const uint32_t qr = rep >> 1, hsh = (rep & 1u) * 16u;
+        const uint32_t hsh = rep * 16u;
 
-        // (1) P̂1 row of D_{t-1}: issue the first probe now, resolve after the ACS
-        uint32_t h1, h2;
-        key_hash(key, NW, h1, h2);
-        uint32_t slot = h1 & a.hmask;
-        const uint32_t fpv = h2 | 1u;
-        const uint32_t f0 = a.fp[slot];
-        const uint32_t* rec0 = a.hrec + (size_t)slot * RW;
-        uint32_t key0[NW];
-#pragma unroll
-        for (int w = 0; w < NW; ++w) key0[w] = rec0[w];
-        const double l0 = reinterpret_cast<const double*>(rec0 + KW)[rr];
-
-        // (2) Eq. 4 for the representatives: A[qp][ns] = (rep 2qp, rep 2qp+1),
-        //     with the Eq. 5 minimum kept in four running accumulators.
-        // Branch metrics: 4 packed words per butterfly, read with scalar loads
-        // (constant address space -> SGPR operands of the packed adds) in
-        // chunks of CH butterflies, software-pipelined one chunk ahead.  Each
-        // chunk pointer is laundered through an asm that depends on the previous
-        // chunk's results, so neither LICM nor the scheduler can hoist the whole
-        // table into SGPRs (which spills).
-        cu32* bmbase = as_const(a.bmp);
-        constexpr int NCH = QP * H / CH;
+        // (2) Eq. 4 for the two representatives, butterfly by butterfly.
+        // Branch metrics: 4 packed words per butterfly, scalar loads from the
+        // constant address space, one 16-word chunk ahead; each chunk pointer
+        // is laundered through an asm that consumes the previous chunk's
+        // outputs, so no pass can hoist the whole table into SGPRs.
+        const uint32_t bb = rep * 2u;
+        const uint32_t lo_sel = bb | ((bb + 1u) << 8), hi_sel = (bb + 4u) | ((bb + 5u) << 8);
+        const uint32_t psel = sw ? (hi_sel | (lo_sel << 16)) : (lo_sel | (hi_sel << 16));
+        constexpr int NCH = H / CH;
         uint32_t bmv[2][4 * CH];
-        uint32_t A[QP][M];
-        us2 mu[QP];
-        us2 m4[4];
         {
           cu32* p0 = bmbase;
-          asm volatile("" : "+s"(p0) : "v"(Dp[0]));   // per-step: not loop invariant
+          asm volatile("" : "+s"(p0) : "v"(Dp[0]));   // per step: not loop invariant
 #pragma unroll
           for (int z = 0; z < 4 * CH; ++z) bmv[0][z] = p0[z];
         }
+        uint32_t P[NG], Dn[NP];
+        us2 m4[4];
+#pragma unroll
+        for (int z = 0; z < 4; ++z) m4[z] = as_us2(0xFFFFFFFFu);
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
-          const int qp = c / (H / CH), j0 = (c % (H / CH)) * CH;
+          const int j0 = c * CH;
           if (c + 1 < NCH) {
-            // the next chunk's pointer depends on every output of the previous
-            // chunk: its scalar loads fly while this chunk computes, and no pass
-            // can pull more of the table forward (or push this chunk's ALU work
-            // past them)
             cu32* pn = bmbase + (c + 1) * CH * 4;
             if (c == 0) {
               asm volatile("" : "+s"(pn) : "v"(Dp[0]));
             } else {
-              const int cp = c - 1, qq = cp / (H / CH), jp = (cp % (H / CH)) * CH;
-              uint32_t* ap = &A[qq][2 * jp];
               static_assert(CH == 4 || H < 4, "chunk barrier written for 4 butterflies");
-              if constexpr (CH == 4) {
-                asm volatile("" : "+s"(pn), "+v"(ap[0]), "+v"(ap[1]), "+v"(ap[2]), "+v"(ap[3]),
-                                  "+v"(ap[4]), "+v"(ap[5]), "+v"(ap[6]), "+v"(ap[7]));
-              }
+              if constexpr (CH == 4)
+                asm volatile("" : "+s"(pn), "+v"(P[(j0 - CH) / 2]), "+v"(P[(j0 - CH) / 2 + 1]));
             }
 #pragma unroll
             for (int z = 0; z < 4 * CH; ++z) bmv[(c + 1) & 1][z] = pn[z];
           }
-          if (j0 == 0) {
+          if (c == NCH / 2) cur.mid(a, rr);          // fingerprint matched: fetch key + row now
 #pragma unroll
-            for (int z = 0; z < 4; ++z) m4[z] = as_us2(0xFFFFFFFFu);
-          }
+          for (int gg = 0; gg < CH / 2; ++gg) {       // group g = states 4g..4g+3 = butterflies 2g, 2g+1
+            const int g = j0 / 2 + gg;
+            uint32_t a4[4];
 #pragma unroll
-          for (int jj = 0; jj < CH; ++jj) {       // butterfly j: preds j, j+H -> 2j, 2j+1
-            const int j = j0 + jj;
-            const uint32_t* b4 = &bmv[c & 1][4 * jj];
-            const us2 pa = as_us2(Dp[j >> 1]), pb = as_us2(Dp[(j + H) >> 1]);
-            const us2 da = (j & 1) ? __builtin_shufflevector(pa, pa, 1, 1) : __builtin_shufflevector(pa, pa, 0, 0);
-            const us2 db = ((j + H) & 1) ? __builtin_shufflevector(pb, pb, 1, 1) : __builtin_shufflevector(pb, pb, 0, 0);
-            const us2 e0 = __builtin_elementwise_min(da + as_us2(b4[0]), db + as_us2(b4[1]));
-            const us2 e1 = __builtin_elementwise_min(da + as_us2(b4[2]), db + as_us2(b4[3]));
-            A[qp][2 * j] = as_u32(e0);
-            A[qp][2 * j + 1] = as_u32(e1);
-            m4[(2 * j) & 3] = __builtin_elementwise_min(m4[(2 * j) & 3], e0);
-            m4[(2 * j + 1) & 3] = __builtin_elementwise_min(m4[(2 * j + 1) & 3], e1);
-          }
-          if (j0 + CH == H)
-            mu[qp] = __builtin_elementwise_min(__builtin_elementwise_min(m4[0], m4[1]),
-                                               __builtin_elementwise_min(m4[2], m4[3]));
-        }
-        // (3) resolve the P̂1 row of D_{t-1} (exact key compare, linear probing)
-        double lpv = a.lp_unseen;
-        {
-          bool eq = f0 == fpv;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) eq = eq && (key0[w] == key[w]);
-          if (eq) {
-            lpv = l0;
-          } else if (f0 != 0u) {
-            for (int pr = 1; pr <= a.max_probe; ++pr) {
-              slot = (slot + 1u) & a.hmask;
-              const uint32_t f = a.fp[slot];
-              if (f == 0u) break;
-              if (f == fpv) {
-                const uint32_t* rc = a.hrec + (size_t)slot * RW;
-                bool e2 = true;
-#pragma unroll
-                for (int w = 0; w < NW; ++w) e2 = e2 && (rc[w] == key[w]);
-                if (e2) { lpv = reinterpret_cast<const double*>(rc + KW)[rr]; break; }
-              }
+            for (int h = 0; h < 2; ++h) {
+              const int j = 2 * g + h, jj = j - j0;
+              const uint32_t* b4 = &bmv[c & 1][4 * jj];
+              const us2 pa = as_us2(Dp[j >> 1]), pb = as_us2(Dp[(j + H) >> 1]);
+              const us2 da = (j & 1) ? __builtin_shufflevector(pa, pa, 1, 1) : __builtin_shufflevector(pa, pa, 0, 0);
+              const us2 db = ((j + H) & 1) ? __builtin_shufflevector(pb, pb, 1, 1) : __builtin_shufflevector(pb, pb, 0, 0);
+              const us2 e0 = __builtin_elementwise_min(da + as_us2(b4[0]), db + as_us2(b4[1]));
+              const us2 e1 = __builtin_elementwise_min(da + as_us2(b4[2]), db + as_us2(b4[3]));
+              a4[2 * h] = as_u32(e0);
+              a4[2 * h + 1] = as_u32(e1);
+              m4[2 * h] = __builtin_elementwise_min(m4[2 * h], e0);
+              m4[2 * h + 1] = __builtin_elementwise_min(m4[2 * h + 1], e1);
             }
+            P[g] = a4[0] | (a4[1] << 4) | (a4[2] << 8) | (a4[3] << 12);
+            // next metric pairs (states 4g, 4g+1) and (4g+2, 4g+3) of the observed rep
+            Dn[2 * g] = __builtin_amdgcn_perm(a4[1], a4[0], psel);
+            Dn[2 * g + 1] = __builtin_amdgcn_perm(a4[3], a4[2], psel);
           }
         }
-        lp += lpv;            // Pd_plotter.py:115, T = P̂1
-        // (4) per group of 4 states: normalised nibble pack P (both reps), its
-        //     pair swap S (the partners r ^ g0), the observed word (-> next key),
-        //     the T_ref comparisons, and the next step's metric pairs.
-        const uint32_t bb = (rep & 1u) * 2u;
-        const uint32_t lo_sel = bb | ((bb + 1u) << 8), hi_sel = (bb + 4u) | ((bb + 5u) << 8);
-        const uint32_t psel = sw ? (hi_sel | (lo_sel << 16)) : (lo_sel | (hi_sel << 16));
-        uint32_t accP[QP], accS[QP];
+        // (3) Eq. 5: subtract the per-rep minimum (nibble-wise, no borrows since
+        //     every nibble >= the minimum; pairs likewise)
+        const us2 mu = __builtin_elementwise_min(__builtin_elementwise_min(m4[0], m4[1]),
+                                                 __builtin_elementwise_min(m4[2], m4[3]));
+        const uint32_t muN = ((uint32_t)mu.x * 0x1111u) | (((uint32_t)mu.y * 0x1111u) << 16);
+        const uint32_t mo = (as_u32(mu) >> hsh) & 0xFFFFu;
+        const us2 mo2 = as_us2(mo * 0x10001u);
 #pragma unroll
-        for (int qp = 0; qp < QP; ++qp) { accP[qp] = 0u; accS[qp] = 0u; }
+        for (int i2 = 0; i2 < NP; ++i2) Dp[i2] = as_u32(as_us2(Dn[i2]) - mo2);
+        // (4) P̂1 row of D_{t-1}
+        const double lpv = cur.resolve(a, key, rr);
+        lp += lpv;            // Pd_plotter.py:115, T = P̂1
+        // (5) per group: normalised P, its pair swap S (partners r ^ g0), the
+        //     T_ref comparisons and the next key.  With obs = half `rep` of
+        //     (sw ? S : P):  c = 1 + [P_rep symmetric] + [P.lo == P.hi] + [S.hi == P.lo]
+        uint32_t acc_sym = 0, acc_eq = 0, acc_x = 0, xs_prev = 0;
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
-          uint32_t Pg[QP], Sg[QP];
-#pragma unroll
-          for (int qp = 0; qp < QP; ++qp) {
-            const us2 mq = mu[qp];
-            const uint32_t y0 = as_u32(as_us2(A[qp][4 * g]) - mq);
-            const uint32_t y1 = as_u32(as_us2(A[qp][4 * g + 1]) - mq);
-            const uint32_t y2 = as_u32(as_us2(A[qp][4 * g + 2]) - mq);
-            const uint32_t y3 = as_u32(as_us2(A[qp][4 * g + 3]) - mq);
-            Pg[qp] = y0 | (y1 << 4) | (y2 << 8) | (y3 << 12);
-            Sg[qp] = ((Pg[qp] << 4) & 0xF0F0F0F0u) | ((Pg[qp] >> 4) & 0x0F0F0F0Fu);
-          }
-          uint32_t x = sw ? Sg[0] : Pg[0];
-#pragma unroll
-          for (int qp = 1; qp < QP; ++qp) x = (qr == (uint32_t)qp) ? (sw ? Sg[qp] : Pg[qp]) : x;
-          const uint32_t o16 = (x >> hsh) & 0xFFFFu;
-          const uint32_t od = o16 * 0x10001u;
-#pragma unroll
-          for (int qp = 0; qp < QP; ++qp) { accP[qp] |= Pg[qp] ^ od; accS[qp] |= Sg[qp] ^ od; }
+          const uint32_t pv = P[g] - muN;
+          const uint32_t sv = ((pv << 4) & 0xF0F0F0F0u) | ((pv >> 4) & 0x0F0F0F0Fu);
+          const uint32_t rot = (pv >> 16) | (pv << 16);
+          acc_sym |= pv ^ sv;
+          acc_eq |= pv ^ rot;
+          acc_x |= sv ^ rot;
+          const uint32_t xs = sw ? sv : pv;
           if (NW == 1) {
-            if (g == 0) key[0] = o16; else key[0] |= o16 << 16;
-          } else {
-            if ((g & 1) == 0) key[g >> 1] = o16; else key[g >> 1] |= o16 << 16;
+            if (NG == 1) key[0] = (xs >> hsh) & 0xFFFFu;
+            else if (g == 1) key[0] = __builtin_amdgcn_perm(xs, xs_prev, lo_sel | ((bb + 4u) << 16) | ((bb + 5u) << 24));
+          } else if (g & 1) {
+            // key word = (half rep of group g-1) | (half rep of group g) << 16
+            key[g >> 1] = __builtin_amdgcn_perm(xs, xs_prev, lo_sel | ((bb + 4u) << 16) | ((bb + 5u) << 24));
           }
-#pragma unroll
-          for (int pi = 2 * g; pi < 2 * g + 2 && pi < NP; ++pi) {
-            uint32_t e0 = A[0][2 * pi], e1 = A[0][2 * pi + 1];
-#pragma unroll
-            for (int qp = 1; qp < QP; ++qp) {
-              e0 = (qr == (uint32_t)qp) ? A[qp][2 * pi] : e0;
-              e1 = (qr == (uint32_t)qp) ? A[qp][2 * pi + 1] : e1;
-            }
-            Dp[pi] = __builtin_amdgcn_perm(e1, e0, psel);   // (D_t(2pi), D_t(2pi+1))
-          }
+          xs_prev = xs;
         }
-        uint32_t c = 0;
-#pragma unroll
-        for (int qp = 0; qp < QP; ++qp)
-          c += ((accP[qp] & 0xFFFFu) == 0u) + ((accP[qp] >> 16) == 0u) + ((accS[qp] & 0xFFFFu) == 0u) +
-               ((accS[qp] >> 16) == 0u);
+        const uint32_t c = 1u + (((acc_sym >> hsh) & 0xFFFFu) == 0u) + ((acc_eq & 0xFFFFu) == 0u) +
+                           ((acc_x >> 16) == 0u);
         lr += s_lt[c];        // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
-        mu_obs = (as_u32(mu[0]) >> hsh) & 0xFFFFu;
-#pragma unroll
-        for (int qp = 1; qp < QP; ++qp) mu_obs = (qr == (uint32_t)qp) ? ((as_u32(mu[qp]) >> hsh) & 0xFFFFu) : mu_obs;
-        ++t;
         if (a.trace) write_trace<m, 1, n>(a.trace, t, a.nseq, q, key);
+        cur.prefetch(a, key, rn);
+        rd.advance();
       }
-      // renormalise the carried metrics once per input word (16-bit headroom)
-      const us2 mud = as_us2(mu_obs * 0x10001u);
-#pragma unroll
-      for (int pi = 0; pi < NP; ++pi) Dp[pi] = as_u32(as_us2(Dp[pi]) - mud);
     }
     if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
   }
@@ -691,7 +716,8 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   if (!kern || !M.d_fp) { set_error("explicit path: unsupported code shape (m,k,n)"); return CVD_E_UNSUPPORTED; }
   if (nseq <= 0) return CVD_OK;
   ExpArgs a;
-  a.fp = M.d_fp; a.hrec = M.d_hrec; a.ltref = M.d_ltref; a.bmp = k1 ? M.d_bmk1 : M.d_bmp;
+  a.fp = M.d_fp; a.hkey = M.d_hkey; a.hrow = M.d_hrow; a.ltref = M.d_ltref;
+  a.bmp = k1 ? M.d_bmk1 : M.d_bmp; a.slot0 = M.slot0;
   a.repmap = M.repmap; a.swmap = M.swmap;
   a.hmask = (uint32_t)(M.hcap - 1); a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
@@ -714,7 +740,8 @@ int cvd::upload_model(cvd_model& M, int device) {
   }
   if (M.hcap > 0) {
     if ((rc = dev_copy(M.d_fp, M.h_fp))) return rc;
-    if ((rc = dev_copy(M.d_hrec, M.h_rec))) return rc;
+    if ((rc = dev_copy(M.d_hkey, M.h_key))) return rc;
+    if ((rc = dev_copy(M.d_hrow, M.h_row))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
     if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
   }
@@ -727,11 +754,11 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_fp, M.d_hrec, M.d_bmp, M.d_bmk1};
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_fp, M.d_hkey, M.d_hrow, M.d_bmp, M.d_bmk1};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
-  M.d_fp = nullptr; M.d_hrec = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
+  M.d_fp = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
   M.device = -1;
   (void)hipSetDevice(cur);
 }
