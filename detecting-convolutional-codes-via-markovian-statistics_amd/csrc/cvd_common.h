@@ -26,20 +26,14 @@ constexpr uint32_t kLearnTag = 0xC0DE1EA7u;
 
 struct U4 { uint32_t x, y, z, w; };
 
-CVD_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __umulhi(a, b);
-#else
-  return (uint32_t)(((uint64_t)a * b) >> 32);
-#endif
-}
-
 // Philox4x32-10 (Salmon et al., SC'11); Random123 known-answer vectors in tests.
 CVD_HD U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = mulhi32(kPhiloxM0, c0), lo0 = kPhiloxM0 * c0;
-    const uint32_t hi1 = mulhi32(kPhiloxM1, c2), lo1 = kPhiloxM1 * c2;
+    // one 32x32->64 multiply per product (v_mad_u64_u32 on gfx950)
+    const uint64_t p0 = (uint64_t)kPhiloxM0 * c0, p1 = (uint64_t)kPhiloxM1 * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += kPhiloxW0; k1 += kPhiloxW1;

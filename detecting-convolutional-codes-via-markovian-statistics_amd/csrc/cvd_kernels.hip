@@ -85,13 +85,33 @@ struct GenArgs {
   uint32_t* r;
 };
 
+// Encoder output for compile-time (k, n): gm[j*k + i] are the tap masks.
+template <int k, int n>
+__device__ __forceinline__ uint32_t enc_out_t(const uint32_t (&gm)[n * k], uint32_t s, uint32_t U) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int i = 0; i < k; ++i) b ^= parity32(gm[j * k + i] & (((U >> i) & 1u) | (s << 1)));
+    o |= b << j;
+  }
+  return o;
+}
+
+// k, n > 0: compile-time shape (only n*k tap masks live); 0, 0: runtime shape.
+template <int kT, int nT>
 __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
   const int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (li >= a.count) return;
   const int64_t q = a.q0 + li;
   const uint64_t sid = (uint64_t)(a.seq_base + li * a.seq_stride);
   const uint32_t slo = (uint32_t)sid, nhi = ctr_hi(sid, kKindNoise), ihi = ctr_hi(sid, kKindInput);
-  const int n = a.enc.n, k = a.enc.k, spw = 32 / n;
+  const int n = nT ? nT : a.enc.n, k = kT ? kT : a.enc.k, spw = 32 / n;
+  constexpr int NK = (kT && nT) ? kT * nT : 1;
+  uint32_t gm[NK];
+#pragma unroll
+  for (int i = 0; i < NK; ++i) gm[i] = a.enc.gmask[i];
   const uint32_t kmask = (1u << k) - 1u;
   const int64_t nwords = (a.N + spw - 1) / spw;
   uint32_t s = 0;
@@ -112,7 +132,11 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
     uint32_t nmask = 0;
     const int64_t g0 = t0 * n, g1 = g0 + (int64_t)ns * n;
     for (int64_t b = g0 >> 2; b <= ((g1 - 1) >> 2); ++b) {
-      const U4 x = philox((uint32_t)b, slo, nhi, a.tag, a.k0, a.k1);
+      // launder the (uniform) key so its 10-round schedule is recomputed by
+      // scalar adds per call instead of being hoisted into spilled SGPRs
+      uint32_t k0 = a.k0, k1 = a.k1;
+      asm volatile("" : "+s"(k0), "+s"(k1));
+      const U4 x = philox((uint32_t)b, slo, nhi, a.tag, k0, k1);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int64_t g = 4 * b + e;
@@ -134,7 +158,9 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
         if (h == 1 && off + (uint32_t)(ns * k) <= 32u) { wv[1] = 0; break; }
         if ((Wh >> 2) != cblk) {
           cblk = Wh >> 2;
-          cval = philox((uint32_t)cblk, slo, ihi, a.tag, a.k0, a.k1);
+          uint32_t k0 = a.k0, k1 = a.k1;
+          asm volatile("" : "+s"(k0), "+s"(k1));
+          cval = philox((uint32_t)cblk, slo, ihi, a.tag, k0, k1);
         }
         wv[h] = u4_get(cval, (uint32_t)(Wh & 3));
       }
@@ -143,8 +169,11 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
     uint32_t word = 0;
     for (int i = 0; i < ns; ++i) {
       const uint32_t U = (ib >> (uint32_t)(i * k)) & kmask;
-      word |= enc_out(a.enc, s, U) << (uint32_t)(n * i);
-      s = enc_next(a.enc, s, U);
+      uint32_t o;
+      if constexpr (kT && nT) o = enc_out_t<kT, nT>(gm, s, U);
+      else o = enc_out(a.enc, s, U);
+      word |= o << (uint32_t)(n * i);
+      s = (U | (s << k)) & ((1u << a.enc.m) - 1u);
     }
     out4[w & 3] = word ^ nmask;
     if ((w & 3) == 3)
@@ -573,7 +602,7 @@ __global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
               m4[2 * h] = __builtin_elementwise_min(m4[2 * h], e0);
               m4[2 * h + 1] = __builtin_elementwise_min(m4[2 * h + 1], e1);
             }
-            P[g] = a4[0] | (a4[1] << 4) | (a4[2] << 8) | (a4[3] << 12);
+            P[g] = (((((a4[3] << 4) | a4[2]) << 4) | a4[1]) << 4) | a4[0];   // 3 x v_lshl_or_b32
             // next metric pairs (states 4g, 4g+1) and (4g+2, 4g+3) of the observed rep
             Dn[2 * g] = __builtin_amdgcn_perm(a4[1], a4[0], psel);
             Dn[2 * g + 1] = __builtin_amdgcn_perm(a4[3], a4[2], psel);
@@ -684,7 +713,11 @@ int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t
   a.random_input = random_input; a.N = N; a.seq_base = seq_base; a.seq_stride = seq_stride;
   a.pitch = pitch; a.q0 = q0; a.count = count; a.r = d_r;
   const unsigned grid = (unsigned)((count + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(gen_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
+  auto kern = gen_kernel<0, 0>;
+  if (enc.k == 1 && enc.n == 2) kern = gen_kernel<1, 2>;
+  else if (enc.k == 1 && enc.n == 3) kern = gen_kernel<1, 3>;
+  else if (enc.k == 2 && enc.n == 3) kern = gen_kernel<2, 3>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
   HIP_CHECK(hipGetLastError());
   return CVD_OK;
 }
