@@ -78,7 +78,8 @@ def main():
     g2 = pkg.Code(cc["gen2"], m, k, n)
     models = {p: det.model(p, a.learn_len if m == 6 else None, 200, 1.0, a.seed) for p in p_grid}
     info = models[p_grid[0]].info()
-    B = a.batch or {"m6": 196_608, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
+    # whole residency rounds: 4 waves/SIMD x 1024 SIMDs x 64 lanes = 262,144 sequences per round
+    B = a.batch or {"m6": 262_144, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
     r = det.stream_buffer(N, 2 * B)
     counts = torch.zeros((len(p_grid), 2), dtype=torch.int64, device=det.device)
     stream = torch.cuda.current_stream()

@@ -47,6 +47,13 @@ typedef const __attribute__((address_space(4))) uint32_t cu32;
 __device__ __forceinline__ cu32* as_const(const uint32_t* p) { return (cu32*)p; }
 
 __device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
+// (a << 4) | b as one v_lshl_or_b32 (the compiler otherwise splits nibble packs
+// into shifts + v_or3)
+__device__ __forceinline__ uint32_t lshl4_or(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
 __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
 
 // Received-word layout in HBM (include/cvd.h): words are grouped in 16-byte
@@ -515,8 +522,13 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
 //   P_g  = raw ACS outputs (<= (ceil(m)+1)n <= 15) nibble-packed, both reps;
 //          the minimum is subtracted once per packed word afterwards
 //   Dn_i = next metric pairs of the observed representative (v_perm_b32)
+#ifndef CVD_K1_WAVES
+#define CVD_K1_WAVES 4
+#endif
+constexpr int kK1WavesPerSimd = CVD_K1_WAVES;   // occupancy target (VGPR budget 512 / waves)
+
 template <int m, int n>
-__global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
+__global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpArgs a) {
   constexpr int M = 1 << m, H = M / 2, R = 1 << n, NG = M / 4, NP = M / 2;
   constexpr int NW = M >= 8 ? M / 8 : 1;
   constexpr int CH = (H >= 4) ? 4 : H;   // butterflies per branch-metric chunk (16 words)
@@ -577,11 +589,24 @@ __global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
               asm volatile("" : "+s"(pn) : "v"(Dp[0]));
             } else {
               static_assert(CH == 4 || H < 4, "chunk barrier written for 4 butterflies");
-              if constexpr (CH == 4)
-                asm volatile("" : "+s"(pn), "+v"(P[(j0 - CH) / 2]), "+v"(P[(j0 - CH) / 2 + 1]));
+              if constexpr (CH == 4) {
+                // every value the previous chunk produced (packed words, next-step
+                // pairs, running minima) is an operand: it must exist here, so no
+                // raw ACS output outlives its chunk
+                const int g0 = (j0 - CH) / 2;
+                asm volatile("" : "+s"(pn), "+v"(P[g0]), "+v"(P[g0 + 1]), "+v"(Dn[2 * g0]),
+                                  "+v"(Dn[2 * g0 + 1]), "+v"(Dn[2 * g0 + 2]), "+v"(Dn[2 * g0 + 3]),
+                                  "+v"(m4[0]), "+v"(m4[1]), "+v"(m4[2]), "+v"(m4[3]));
+              }
             }
+#ifdef CVD_EXPERIMENT_CONST_BM
+#pragma unroll
+            for (int z = 0; z < 4 * CH; ++z) bmv[(c + 1) & 1][z] = 0x00010001u * ((z + c) % 3);
+            (void)pn;
+#else
 #pragma unroll
             for (int z = 0; z < 4 * CH; ++z) bmv[(c + 1) & 1][z] = pn[z];
+#endif
           }
           if (c == NCH / 2) cur.mid(a, rr);          // fingerprint matched: fetch key + row now
 #pragma unroll
@@ -602,7 +627,7 @@ __global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
               m4[2 * h] = __builtin_elementwise_min(m4[2 * h], e0);
               m4[2 * h + 1] = __builtin_elementwise_min(m4[2 * h + 1], e1);
             }
-            P[g] = (((((a4[3] << 4) | a4[2]) << 4) | a4[1]) << 4) | a4[0];   // 3 x v_lshl_or_b32
+            P[g] = lshl4_or(lshl4_or(lshl4_or(a4[3], a4[2]), a4[1]), a4[0]);
             // next metric pairs (states 4g, 4g+1) and (4g+2, 4g+3) of the observed rep
             Dn[2 * g] = __builtin_amdgcn_perm(a4[1], a4[0], psel);
             Dn[2 * g + 1] = __builtin_amdgcn_perm(a4[3], a4[2], psel);
@@ -623,13 +648,16 @@ __global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
         // (5) per group: normalised P, its pair swap S (partners r ^ g0), the
         //     T_ref comparisons and the next key.  With obs = half `rep` of
         //     (sw ? S : P):  c = 1 + [P_rep symmetric] + [P.lo == P.hi] + [S.hi == P.lo]
+        // (nibble pairs 2i, 2i+1 equal  <=>  (pv ^ pv >> 4) & 0x0F0F0F0F == 0, per half)
         uint32_t acc_sym = 0, acc_eq = 0, acc_x = 0, xs_prev = 0;
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
           const uint32_t pv = P[g] - muN;
-          const uint32_t sv = ((pv << 4) & 0xF0F0F0F0u) | ((pv >> 4) & 0x0F0F0F0Fu);
-          const uint32_t rot = (pv >> 16) | (pv << 16);
-          acc_sym |= pv ^ sv;
+          const uint32_t lsr = pv >> 4;
+          uint32_t sv = ((pv << 4) & 0xF0F0F0F0u) | (lsr & 0x0F0F0F0Fu);
+          asm("" : "+v"(sv));   // keep the one v_bfi_b32 (else re-expanded into and/and/bitop3 per use)
+          const uint32_t rot = __builtin_amdgcn_alignbit(pv, pv, 16);
+          acc_sym |= pv ^ lsr;
           acc_eq |= pv ^ rot;
           acc_x |= sv ^ rot;
           const uint32_t xs = sw ? sv : pv;
@@ -642,7 +670,7 @@ __global__ __launch_bounds__(kBlock) void detect_k1_kernel(ExpArgs a) {
           }
           xs_prev = xs;
         }
-        const uint32_t c = 1u + (((acc_sym >> hsh) & 0xFFFFu) == 0u) + ((acc_eq & 0xFFFFu) == 0u) +
+        const uint32_t c = 1u + ((((acc_sym & 0x0F0F0F0Fu) >> hsh) & 0xFFFFu) == 0u) + ((acc_eq & 0xFFFFu) == 0u) +
                            ((acc_x >> 16) == 0u);
         lr += s_lt[c];        // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
         if (a.trace) write_trace<m, 1, n>(a.trace, t, a.nseq, q, key);
