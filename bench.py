@@ -165,7 +165,8 @@ def main():
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "detect_k1_kernel<6,2> (k=1 orbit explicit path)" if m == 6 else "detect kernel",
+                     "kernel": (pkg.KERNEL_NAMES[info["explicit_kernel"]] if info["kind"]
+                                else "detect_table_kernel (enumerated state automaton)"),
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,

@@ -12,9 +12,9 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
-PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC = 0, 1, 2, 3
+PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT = 0, 1, 2, 3, 4
 
 
 class CvdError(RuntimeError):
@@ -38,7 +38,13 @@ class cvd_model_info(ctypes.Structure):
                 ("m", ctypes.c_int32), ("S", ctypes.c_int64), ("n_rows", ctypes.c_int64),
                 ("learn_len_eff", ctypes.c_int64), ("hash_capacity", ctypes.c_int64),
                 ("max_probe", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("logp1_unseen", ctypes.c_double)]
+                ("logp1_unseen", ctypes.c_double), ("explicit_kernel", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+KERNEL_NAMES = {0: "none", 1: "detect_explicit_kernel (generic explicit path)",
+                2: "detect_k1_kernel (k=1 orbit explicit path)",
+                3: "detect_k1b_kernel (k=1 butterfly explicit path)"}
 
 
 EXPORTS = {

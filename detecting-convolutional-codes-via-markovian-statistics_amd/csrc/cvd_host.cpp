@@ -378,6 +378,8 @@ void build_hash(cvd_model& Mo) {
   std::vector<uint32_t> kw((size_t)nw);
   for (int64_t i = 0; i < Mo.n_rows; ++i) {
     pack_nibbles(Mo.keys.data() + (size_t)i * M, M, kw.data());
+    if (M >= 8)
+      for (int w = 0; w < nw; ++w) kw[w] = key_swap(kw[w]);   // device key layout
     uint32_t h1, h2;
     key_hash(kw.data(), nw, h1, h2);
     uint64_t slot = h1 & (uint64_t)(cap - 1);
@@ -427,9 +429,34 @@ void build_bmk1(cvd_model& Mo, const Tabs& T) {
   Mo.k1_ok = true;
 }
 
+void build_bfly(cvd_model& Mo, const Tabs& T) {
+  // Standard butterfly: out(j, 1) = out(j, 0) ^ 3 and out(j + 2^(m-1), u) =
+  // out(j, u) ^ 3 for every j (tap-0 and tap-m columns both 11).  Then the two
+  // ACS candidates of states (2j, 2j+1) carry metrics (e, 2-e) and (2-e, e),
+  // e = popcount(out(j, 0) ^ y).
+  if (T.k != 1 || T.n != 2 || T.m < 3) return;
+  const int H = T.M / 2;
+  for (int j = 0; j < H; ++j) {
+    const uint32_t x = T.out[j * T.K + 0];
+    if (T.out[j * T.K + 1] != (x ^ 3u) || T.out[(j + H) * T.K + 0] != (x ^ 3u) ||
+        T.out[(j + H) * T.K + 1] != x)
+      return;
+  }
+  Mo.bfly.assign((size_t)H, 0u);
+  Mo.bfly_uni = 1u;
+  for (int j = 0; j < H; ++j) {
+    const uint32_t x = T.out[j * T.K + 0];
+    for (uint32_t y = 0; y < 4; ++y) Mo.bfly[(size_t)j] |= (uint32_t)__builtin_popcount(x ^ y) << (8 * y);
+    // class of out(j, 0): {00, 11} or {01, 10}; out(0, 0) = 00
+    if (__builtin_popcount(x) & 1) Mo.bfly_uni = 0u;
+  }
+  Mo.k1b_ok = true;
+}
+
 void build_bmp(cvd_model& Mo, const Tabs& T) {
   if (!explicit_supported(T.m, T.k, T.n)) return;
   build_bmk1(Mo, T);
+  build_bfly(Mo, T);
   const int QP = T.R / 2;
   Mo.bmp.assign((size_t)QP * T.M * T.K, 0u);
   for (int qp = 0; qp < QP; ++qp)
@@ -587,6 +614,8 @@ extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
   info->max_probe = Mo->max_probe;
   info->device = Mo->device;
   info->logp1_unseen = Mo->logp1_unseen;
+  info->explicit_kernel = explicit_kernel_of(*Mo);
+  info->reserved = 0;
   return CVD_OK;
 }
 

@@ -41,6 +41,11 @@ struct cvd_model {
   bool k1_ok = false;
   uint32_t repmap = 0, swmap = 0;  // rep index of r (4 bits per r), r > r ^ g0 (1 bit per r)
   std::vector<uint32_t> bmk1;      // [reps/2][2^m][2] packed (bm(rep 2qp), bm(rep 2qp+1))
+  // k = 1, n = 2 single-vector kernel (standard butterfly: tap-0 and tap-m columns
+  // both 11): per butterfly j, byte y of bfly[j] = popcount(out(j, 0) ^ y)
+  bool k1b_ok = false;
+  uint32_t bfly_uni = 0;           // every out(j, 0), j < 2^(m-1), in {00, 11}
+  std::vector<uint32_t> bfly;      // [2^m / 2]
 
   // device copies
   int device = -1;
@@ -52,6 +57,7 @@ struct cvd_model {
   uint32_t* d_hrow = nullptr;
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
+  uint32_t* d_bfly = nullptr;
 };
 
 namespace cvd {
@@ -63,6 +69,19 @@ CVD_HD int row_words(int n) { return (3 * (1 << n) + 3) & ~3; }
 
 // Nibble packing of a metric vector: state s in nibble s (word s / 8, bits 4*(s % 8)).
 void pack_nibbles(const uint8_t* D, int M, uint32_t* out);
+
+// Device key layout (hash keys, row cursor) for 2^m >= 8: inside each 32-bit
+// word, state 8w + s sits in nibble bitrev3(s) -- the order in which a lane's
+// packed (D(2j), D(2j+1)) pairs collapse into nibbles with two shift-adds.
+// key_swap converts either way (an involution: nibbles 1 <-> 4, 3 <-> 6).
+CVD_HD uint32_t key_swap(uint32_t w) {
+  const uint32_t t = (w ^ (w >> 12)) & 0x0000F0F0u;
+  return w ^ t ^ (t << 12);
+}
+CVD_HD int key_nibble(int M, int s) {   // nibble index of state s within its word
+  const int b = s & 7;
+  return M >= 8 ? (((b & 1) << 2) | (b & 2) | ((b >> 2) & 1)) : b;
+}
 
 // 32-bit hash pair of a nibble-packed key; must match the device version.
 // A rotate/xor-add fold (2 full-rate VALU ops per word) and two finalising
@@ -85,8 +104,12 @@ int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int6
                         int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream);
 int launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                            int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
-                           void* stream, bool allow_k1);
+                           void* stream, int variant);
+// launch_detect_explicit variants
+constexpr int kExplicitBest = 0, kExplicitOrbit = 1, kExplicitGeneric = 2;
 int upload_model(cvd_model& M, int device);
+// CVD_KERNEL_* that launch_detect_explicit(kExplicitBest) picks for this model
+int explicit_kernel_of(const cvd_model& M);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);
 

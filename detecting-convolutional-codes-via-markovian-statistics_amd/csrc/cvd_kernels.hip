@@ -253,6 +253,7 @@ struct ExpArgs {
   const double* ltref;      // [R + 1]
   const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
+  uint32_t bfly_uni;        // k = 1 butterfly kernel: every out(j, 0), j < 2^(m-1), in one class
   uint32_t hmask;
   int32_t max_probe;
   int32_t slot0;            // slot of D_0 = 0
@@ -401,13 +402,22 @@ struct Shape {
   static_assert(m >= 2 && k <= m && n >= 1, "explicit path shape");
 };
 
-template <int m, int k, int n>
+// D_t of one sequence as 2^m bytes (canonical state order); kDev: Dw is in the
+// device key layout (key_nibble), else canonical nibbles
+template <int m, int k, int n, bool kDev>
 __device__ __forceinline__ void write_trace(uint8_t* tr, int64_t t, int64_t nseq, int64_t q,
                                             const uint32_t (&Dw)[Shape<m, k, n>::NW]) {
   using S = Shape<m, k, n>;
   uint8_t* o = tr + ((size_t)t * nseq + q) * S::M;
 #pragma unroll
-  for (int s = 0; s < S::M; ++s) o[s] = (uint8_t)((Dw[s >> 3] >> (4 * (s & 7))) & 15u);
+  for (int s = 0; s < S::M; ++s)
+    o[s] = (uint8_t)((Dw[s >> 3] >> (4 * (kDev ? key_nibble(S::M, s) : (s & 7)))) & 15u);
+}
+
+template <int NW, int M>
+__device__ __forceinline__ void to_key_layout(const uint32_t (&Dw)[NW], uint32_t (&K)[NW]) {
+#pragma unroll
+  for (int w = 0; w < NW; ++w) K[w] = M >= 8 ? key_swap(Dw[w]) : Dw[w];
 }
 
 template <int m, int k, int n>
@@ -423,7 +433,9 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
     uint32_t Dw[S::NW];
 #pragma unroll
     for (int w = 0; w < S::NW; ++w) Dw[w] = 0u;
-    if (a.trace) write_trace<m, k, n>(a.trace, 0, a.nseq, q, Dw);
+    uint32_t Kw[S::NW];   // Dw in the device key layout (hash keys)
+    to_key_layout<S::NW, S::M>(Dw, Kw);
+    if (a.trace) write_trace<m, k, n, false>(a.trace, 0, a.nseq, q, Dw);
     StreamReader<n> rd;
     rd.init(a.r, a.nseq, q, a.N);
     RowCursor<S::NW, S::R> cur;
@@ -481,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
           c += ((acc & 0xFFFFu) == 0u) + ((acc >> 16) == 0u);
         }
         // (4) P̂1 row of D_{t-1}
-        const double lpv = cur.resolve(a, Dw, rr);
+        const double lpv = cur.resolve(a, Kw, rr);
         lp += lpv;            // Pd_plotter.py:115 with T = P̂1
         lr += s_lt[c];        // Pd_plotter.py:115 with T = T_ref(1/2) = c / 2^n
         // (5) D_t becomes the state
@@ -491,8 +503,9 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
 #pragma unroll
           for (int w = 0; w < S::NW; ++w) Dw[w] = obs[2 * w] | (obs[2 * w + 1] << 16);
         }
-        if (a.trace) write_trace<m, k, n>(a.trace, t, a.nseq, q, Dw);
-        cur.prefetch(a, Dw, rn);
+        to_key_layout<S::NW, S::M>(Dw, Kw);
+        if (a.trace) write_trace<m, k, n, false>(a.trace, t, a.nseq, q, Dw);
+        cur.prefetch(a, Kw, rn);
         rd.advance();
       }
     }
@@ -546,7 +559,7 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
     uint32_t key[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) key[w] = 0u;
-    if (a.trace) write_trace<m, 1, n>(a.trace, 0, a.nseq, q, key);
+    if (a.trace) write_trace<m, 1, n, true>(a.trace, 0, a.nseq, q, key);
     cu32* bmbase = as_const(a.bmp);
     StreamReader<n> rd;
     rd.init(a.r, a.nseq, q, a.N);
@@ -577,9 +590,7 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
           for (int z = 0; z < 4 * CH; ++z) bmv[0][z] = p0[z];
         }
         uint32_t P[NG], Dn[NP];
-        us2 m4[4];
-#pragma unroll
-        for (int z = 0; z < 4; ++z) m4[z] = as_us2(0xFFFFFFFFu);
+        uint32_t zn = 0u;   // per-half "some raw nibble is 0" flags (bit 3 of each nibble)
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
           const int j0 = c * CH;
@@ -596,7 +607,7 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
                 const int g0 = (j0 - CH) / 2;
                 asm volatile("" : "+s"(pn), "+v"(P[g0]), "+v"(P[g0 + 1]), "+v"(Dn[2 * g0]),
                                   "+v"(Dn[2 * g0 + 1]), "+v"(Dn[2 * g0 + 2]), "+v"(Dn[2 * g0 + 3]),
-                                  "+v"(m4[0]), "+v"(m4[1]), "+v"(m4[2]), "+v"(m4[3]));
+                                  "+v"(zn));
               }
             }
 #ifdef CVD_EXPERIMENT_CONST_BM
@@ -624,21 +635,23 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
               const us2 e1 = __builtin_elementwise_min(da + as_us2(b4[2]), db + as_us2(b4[3]));
               a4[2 * h] = as_u32(e0);
               a4[2 * h + 1] = as_u32(e1);
-              m4[2 * h] = __builtin_elementwise_min(m4[2 * h], e0);
-              m4[2 * h + 1] = __builtin_elementwise_min(m4[2 * h + 1], e1);
             }
             P[g] = lshl4_or(lshl4_or(lshl4_or(a4[3], a4[2]), a4[1]), a4[0]);
+            // zero-nibble test per 16-bit half (packed subtract: no borrow across halves)
+            zn |= as_u32(as_us2(P[g]) - as_us2(0x11111111u)) & ~P[g];
             // next metric pairs (states 4g, 4g+1) and (4g+2, 4g+3) of the observed rep
             Dn[2 * g] = __builtin_amdgcn_perm(a4[1], a4[0], psel);
             Dn[2 * g + 1] = __builtin_amdgcn_perm(a4[3], a4[2], psel);
           }
         }
         // (3) Eq. 5: subtract the per-rep minimum (nibble-wise, no borrows since
-        //     every nibble >= the minimum; pairs likewise)
-        const us2 mu = __builtin_elementwise_min(__builtin_elementwise_min(m4[0], m4[1]),
-                                                 __builtin_elementwise_min(m4[2], m4[3]));
-        const uint32_t muN = ((uint32_t)mu.x * 0x1111u) | (((uint32_t)mu.y * 0x1111u) << 16);
-        const uint32_t mo = (as_u32(mu) >> hsh) & 0xFFFFu;
+        //     every nibble >= the minimum; pairs likewise).  For n = 2 the minimum
+        //     is 0 or 1: D_{t-1} has a 0 state, and of its two branches (outputs o,
+        //     o ^ g0, g0 != 0) one has metric <= 1.  So mu = [no nibble is 0].
+        const uint32_t zm = zn & 0x88888888u;
+        const uint32_t mu_lo = (zm & 0xFFFFu) == 0u, mu_hi = (zm >> 16) == 0u;
+        const uint32_t muN = (mu_lo * 0x1111u) | (mu_hi * 0x11110000u);
+        const uint32_t mo = rep ? mu_hi : mu_lo;
         const us2 mo2 = as_us2(mo * 0x10001u);
 #pragma unroll
         for (int i2 = 0; i2 < NP; ++i2) Dp[i2] = as_u32(as_us2(Dn[i2]) - mo2);
@@ -673,7 +686,11 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
         const uint32_t c = 1u + ((((acc_sym & 0x0F0F0F0Fu) >> hsh) & 0xFFFFu) == 0u) + ((acc_eq & 0xFFFFu) == 0u) +
                            ((acc_x >> 16) == 0u);
         lr += s_lt[c];        // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
-        if (a.trace) write_trace<m, 1, n>(a.trace, t, a.nseq, q, key);
+        if constexpr (M >= 8) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) key[w] = key_swap(key[w]);   // device key layout
+        }
+        if (a.trace) write_trace<m, 1, n, true>(a.trace, t, a.nseq, q, key);
         cur.prefetch(a, key, rn);
         rd.advance();
       }
@@ -683,7 +700,153 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
 
+// ──────── k = 1, n = 2 single-vector kernel (standard butterfly; m = 6 headline) ────────
+//
+// For codes whose tap-0 and tap-m columns are both 11 (every good rate-1/2 code,
+// (133,171) and (7,5) included), the two ACS candidates of new states (2j, 2j+1)
+// come from D(j) with metrics (e, 2-e) and from D(j + 2^(m-1)) with (2-e, e),
+// e = popcount(out(j, 0) ^ y).  The lane's own received word y picks e per
+// butterfly with ONE v_perm_b32 from a 4-byte constant, and one packed-16
+// add/add/min produces the pair (D(2j), D(2j+1)) -- the next step's operand, in
+// place.  Only D_t(y) itself is computed: 2^(m-1) butterflies of 4 packed VALU
+// ops, against 2 x 2^m ACS for the orbit kernel.
+//
+// T_ref count without the other words (exact, no fallback).  y ^ 3 flips every
+// e to 2 - e, so D_t(y ^ 3) is the pair swap of D_t(y).  For y' = y ^ 1 or
+// y ^ 2 the butterfly classes swap (e in {0, 2} <-> e' = 1), and in each
+// butterfly the word with e in {0, 2} must give A(2j) == A(2j+1), which holds
+// iff D_{t-1}(j) == D_{t-1}(j + 2^(m-1)).  So D_t(y') == D_t(y) (up to the
+// normalisation) needs equal halves; with equal halves d_j, A(2j) = A(2j+1) =
+// d_j + [e_j == 1] under y and d_j + [e_j != 1] under y', equal up to a constant
+// iff [e_j == 1] is constant over j, i.e. every out(j, 0) is in one class
+// (a property of the code only: bfly_uni).  Hence
+// c = 1 + [D_t(y) == pair swap] + 2 [halves equal and bfly_uni].
+//
+// Dp carries the metric pairs plus a per-lane offset O (the sum of the step
+// minima since the last renormalisation, every kRenorm steps); nibble keys are
+// formed with two shift-adds per 4 butterflies and the offset removed by one
+// subtraction per word (exact modulo 2^32).  The step minimum is 0 or 1
+// (n = 2; D_{t-1} has a 0 state and one of its branches has metric <= 1), so it
+// is read off a zero-nibble test.
+#ifndef CVD_K1B_WAVES
+#define CVD_K1B_WAVES 4
+#endif
+constexpr int kK1bWavesPerSimd = CVD_K1B_WAVES;
+constexpr int kRenorm = 128;   // O <= 128: raw pair values stay < 256 (byte packing)
+
+// The common step: D_t(y) for the lane's own word, in place in Dp (pair i is
+// dead once butterflies 2i, 2i + 1 and 2i - H, 2i + 1 - H have read it), and
+// the nibble keys of the raw metrics minus the running offset.
+template <int m>
+__device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1 << m) / 8, 4>& cur, uint32_t rr,
+                                        uint32_t (&Dp)[(1 << m) / 2], uint32_t (&kw)[(1 << m) / 8],
+                                        uint32_t sel, uint32_t O8, uint32_t& zn) {
+  constexpr int M = 1 << m, H = M / 2;
+  uint32_t E[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    if (j == H / 2) cur.mid(a, rr);     // fingerprint matched: key + row loads under the second half
+    const uint32_t T = tb[j];
+    const us2 pa = as_us2(Dp[j >> 1]), pb = as_us2(Dp[(j >> 1) + H / 2]);
+    const us2 da = (j & 1) ? __builtin_shufflevector(pa, pa, 1, 1) : __builtin_shufflevector(pa, pa, 0, 0);
+    const us2 db = (j & 1) ? __builtin_shufflevector(pb, pb, 1, 1) : __builtin_shufflevector(pb, pb, 0, 0);
+    const us2 W = as_us2(__builtin_amdgcn_perm(T, T, sel));   // (e, 2 - e)
+    E[j] = as_u32(__builtin_elementwise_min(da + W, db + __builtin_shufflevector(W, W, 1, 0)));
+    if ((j & 3) == 3) {
+      // word w = states 8w..8w+7 in nibble order bitrev3 (device key layout)
+      const uint32_t x = E[j - 3] + (E[j - 2] << 8);
+      const uint32_t y = E[j - 1] + (E[j] << 8);
+      const uint32_t v = x + (y << 4) - O8;             // nibbles = raw metric - offset <= 14
+      zn |= (v - 0x11111111u) & ~v;
+      kw[j >> 2] = v;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < H; ++j) Dp[j] = E[j];
+}
+
+template <int m>
+__global__ __launch_bounds__(kBlock, kK1bWavesPerSimd) void detect_k1b_kernel(ExpArgs a) {
+  constexpr int M = 1 << m, H = M / 2, NW = M / 8, R = 4;
+  static_assert(m >= 3, "k1b kernel: 2^m >= 8 (whole key words)");
+  __shared__ double s_lt[R + 1];
+  if (threadIdx.x <= R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  __syncthreads();
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = q < a.nseq;
+  double lp = 0.0, lr = 0.0;
+  if (valid) {
+    uint32_t Dp[H];   // (D(2i), D(2i+1)) + O, packed 16-bit
+#pragma unroll
+    for (int i = 0; i < H; ++i) Dp[i] = 0u;
+    uint32_t key[NW];  // normalised D_{t-1}, device key layout
+#pragma unroll
+    for (int w = 0; w < NW; ++w) key[w] = 0u;
+    uint32_t O = 0u, O8 = 0u;   // O8 = O * 0x11111111
+    if (a.trace) write_trace<m, 1, 2, true>(a.trace, 0, a.nseq, q, key);
+    StreamReader<2> rd;
+    rd.init(a.r, a.nseq, q, a.N);
+    RowCursor<NW, R> cur;
+    cur.start(a, rd.peek());
+    for (int64_t t = 1; t <= a.N; ++t) {
+      const uint32_t rr = rd.peek();
+      const uint32_t rn = t < a.N ? rd.peek_next() : 0u;
+      // halves test: D_{t-1}(j) == D_{t-1}(j + 2^(m-1)) for every j
+      uint32_t hx = 0u;
+      if constexpr (NW >= 2) {
+#pragma unroll
+        for (int w = 0; w < NW / 2; ++w) hx |= key[w] ^ key[w + NW / 2];
+      } else {
+        hx = (key[0] ^ (key[0] >> 4)) & 0x0F0F0F0Fu;   // states s, s + 4 = nibbles 2i, 2i + 1
+      }
+      const uint32_t sel = rr | ((rr ^ 3u) << 16) | 0x0C000C00u;
+      cu32* tb = as_const(a.bmp);
+      asm volatile("" : "+s"(tb));   // per step: the table is re-read (scalar cache), not held in SGPRs
+      uint32_t kw[NW];
+      uint32_t zn = 0u;
+      k1b_acs<m>(a, tb, cur, rr, Dp, kw, sel, O8, zn);
+      // Eq. 5: step minimum 0 or 1
+      const uint32_t mu = (zn & 0x88888888u) == 0u;
+      const uint32_t mu8 = mu ? 0x11111111u : 0u;
+      O += mu;
+      O8 += mu8;
+      // P̂1 row of D_{t-1}
+      lp += cur.resolve(a, key, rr);          // Pd_plotter.py:115, T = P̂1
+      uint32_t sym = 0u;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        key[w] = kw[w] - mu8;
+        sym |= key[w] ^ (key[w] >> 16);        // pairs (2j, 2j+1) = nibbles i, i + 4
+      }
+      // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni
+      const uint32_t c = 1u + ((sym & 0xFFFFu) == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
+      lr += s_lt[c];                          // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
+      if (a.trace) write_trace<m, 1, 2, true>(a.trace, t, a.nseq, q, key);
+      cur.prefetch(a, key, rn);
+      rd.advance();
+      if ((t & (kRenorm - 1)) == 0) {
+        const us2 o2 = as_us2(O * 0x10001u);
+#pragma unroll
+        for (int i = 0; i < H; ++i) Dp[i] = as_u32(as_us2(Dp[i]) - o2);
+        O = 0u;
+        O8 = 0u;
+      }
+    }
+    if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+  }
+  count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
+}
+
 using ExpKernel = void (*)(ExpArgs);
+ExpKernel pick_k1b(int m) {
+  switch (m) {
+    case 3: return detect_k1b_kernel<3>;
+    case 4: return detect_k1b_kernel<4>;
+    case 5: return detect_k1b_kernel<5>;
+    case 6: return detect_k1b_kernel<6>;
+  }
+  return nullptr;
+}
 ExpKernel pick_k1(int m, int n) {
   if (n == 2) {
     switch (m) {
@@ -769,17 +932,36 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
   return CVD_OK;
 }
 
+// Kernel of the explicit path: the butterfly kernel when the code has standard
+// butterflies, else the orbit kernel (k = 1), else the generic one.
+static int select_explicit(const cvd_model& M, int variant, ExpKernel* kern, const uint32_t** bmp) {
+  if (variant == cvd::kExplicitBest && M.k1b_ok)
+    if (ExpKernel k = pick_k1b(M.dec.m)) { *kern = k; *bmp = M.d_bfly; return CVD_KERNEL_BUTTERFLY; }
+  if (variant != cvd::kExplicitGeneric && M.k1_ok)
+    if (ExpKernel k = pick_k1(M.dec.m, M.dec.n)) { *kern = k; *bmp = M.d_bmk1; return CVD_KERNEL_ORBIT; }
+  if (ExpKernel k = pick_explicit(M.dec.m, M.dec.k, M.dec.n)) { *kern = k; *bmp = M.d_bmp; return CVD_KERNEL_GENERIC; }
+  *kern = nullptr; *bmp = nullptr;
+  return CVD_KERNEL_NONE;
+}
+
+int cvd::explicit_kernel_of(const cvd_model& M) {
+  ExpKernel k;
+  const uint32_t* b;
+  return select_explicit(M, kExplicitBest, &k, &b);
+}
+
 int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                                 int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
-                                void* stream, bool allow_k1) {
-  ExpKernel k1 = (allow_k1 && M.k1_ok && M.d_bmk1) ? pick_k1(M.dec.m, M.dec.n) : nullptr;
-  ExpKernel kern = k1 ? k1 : pick_explicit(M.dec.m, M.dec.k, M.dec.n);
-  if (!kern || !M.d_fp) { set_error("explicit path: unsupported code shape (m,k,n)"); return CVD_E_UNSUPPORTED; }
+                                void* stream, int variant) {
+  ExpKernel kern = nullptr;
+  const uint32_t* bmp = nullptr;
+  select_explicit(M, variant, &kern, &bmp);
+  if (!kern || !M.d_fp || !bmp) { set_error("explicit path: unsupported code shape (m,k,n)"); return CVD_E_UNSUPPORTED; }
   if (nseq <= 0) return CVD_OK;
   ExpArgs a;
   a.fp = M.d_fp; a.hkey = M.d_hkey; a.hrow = M.d_hrow; a.ltref = M.d_ltref;
-  a.bmp = k1 ? M.d_bmk1 : M.d_bmp; a.slot0 = M.slot0;
-  a.repmap = M.repmap; a.swmap = M.swmap;
+  a.bmp = bmp; a.slot0 = M.slot0;
+  a.repmap = M.repmap; a.swmap = M.swmap; a.bfly_uni = M.bfly_uni;
   a.hmask = (uint32_t)(M.hcap - 1); a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   a.trace = d_trace;
@@ -805,6 +987,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_hrow, M.h_row))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
     if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
+    if ((rc = dev_copy(M.d_bfly, M.bfly))) return rc;
   }
   M.device = device;
   return CVD_OK;
@@ -815,11 +998,12 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_fp, M.d_hkey, M.d_hrow, M.d_bmp, M.d_bmk1};
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_fp, M.d_hkey, M.d_hrow, M.d_bmp, M.d_bmk1, M.d_bfly};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
   M.d_fp = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
+  M.d_bfly = nullptr;
   M.device = -1;
   (void)hipSetDevice(cur);
 }
@@ -874,9 +1058,10 @@ extern "C" int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N
   if (rc) return rc;
   if (path == CVD_PATH_AUTO) path = model->kind == 0 ? CVD_PATH_TABLE : CVD_PATH_EXPLICIT;
   if (path == CVD_PATH_TABLE) return launch_detect_table(*model, d_r, N, nseq, n_h1, d_sums, d_counts, stream);
-  if (path == CVD_PATH_EXPLICIT || path == CVD_PATH_EXPLICIT_GENERIC)
+  if (path == CVD_PATH_EXPLICIT || path == CVD_PATH_EXPLICIT_GENERIC || path == CVD_PATH_EXPLICIT_ORBIT)
     return launch_detect_explicit(*model, d_r, N, nseq, n_h1, d_sums, d_counts, nullptr, stream,
-                                  path == CVD_PATH_EXPLICIT);
+                                  path == CVD_PATH_EXPLICIT ? kExplicitBest
+                                  : path == CVD_PATH_EXPLICIT_ORBIT ? kExplicitOrbit : kExplicitGeneric);
   set_error("unknown path");
   return CVD_E_INVALID;
 }
@@ -893,7 +1078,7 @@ extern "C" int cvd_trace(const cvd_model* model, const uint32_t* d_r, int64_t N,
   int64_t* d_tmp = nullptr;
   HIP_CHECK(hipMallocAsync((void**)&d_tmp, 2 * sizeof(int64_t), (hipStream_t)stream));
   HIP_CHECK(hipMemsetAsync(d_tmp, 0, 2 * sizeof(int64_t), (hipStream_t)stream));
-  rc = launch_detect_explicit(*model, d_r, N, nseq, 0, nullptr, d_tmp, d_D, stream, true);
+  rc = launch_detect_explicit(*model, d_r, N, nseq, 0, nullptr, d_tmp, d_D, stream, kExplicitBest);
   (void)hipFreeAsync(d_tmp, (hipStream_t)stream);
   return rc;
 }

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 1
+#define CVD_ABI_VERSION 2
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -67,7 +67,14 @@ typedef struct cvd_model_info {
   int32_t max_probe;       /* longest probe sequence in the hash */
   int32_t device;          /* device holding the tables, -1 if not uploaded */
   double logp1_unseen;     /* log P̂1 of a row never visited (sparse models) */
+  int32_t explicit_kernel; /* kernel CVD_PATH_EXPLICIT launches: CVD_KERNEL_* */
+  int32_t reserved;
 } cvd_model_info;
+
+#define CVD_KERNEL_NONE 0       /* explicit path unsupported for this shape */
+#define CVD_KERNEL_GENERIC 1    /* detect_explicit_kernel<m,k,n>: ACS for every received word */
+#define CVD_KERNEL_ORBIT 2      /* detect_k1_kernel<m,n>: k = 1, ACS for the 2^n/2 orbit representatives */
+#define CVD_KERNEL_BUTTERFLY 3  /* detect_k1b_kernel<m>: k = 1, n = 2 standard butterflies, one ACS vector */
 
 typedef struct cvd_model cvd_model;
 
@@ -118,8 +125,9 @@ int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int
 
 #define CVD_PATH_AUTO 0
 #define CVD_PATH_TABLE 1     /* enumerated state automaton (dense models) */
-#define CVD_PATH_EXPLICIT 2  /* explicit 2^m metric vector + hashed P̂1 rows (k=1 orbit kernel when possible) */
+#define CVD_PATH_EXPLICIT 2  /* explicit 2^m metric vector + hashed P̂1 rows (fastest k=1 kernel that applies) */
 #define CVD_PATH_EXPLICIT_GENERIC 3  /* explicit path, ACS for every received word (no orbit reduction) */
+#define CVD_PATH_EXPLICIT_ORBIT 4    /* explicit path, k=1 two-representative orbit kernel */
 
 /* Detector over sequences 0..nseq-1 (pitch = nseq): per sequence the sequential
  * fp64 sums log P̂1(D_0^N) and log T_ref(D_0^N) (Pd_plotter.py:106-116); sequences

@@ -248,17 +248,36 @@ def test_m6_full_size_properties(pkg, dev):
                                              ("m6_133_171", "m6_171_133", 1500, 0.05),
                                              ("m6_133_171", "m6_171_133", 333, 0.2)])
 def test_orbit_kernel_equals_generic_explicit(pkg, golden, dev, name, g2name, N, p):
-    """k = 1 orbit kernel (ACS only for r < r ^ g0) == generic explicit kernel
-    (ACS for every received word) == table automaton (dense codes)."""
+    """k = 1 butterfly kernel (default explicit path) == k = 1 orbit kernel (ACS
+    only for r < r ^ g0) == generic explicit kernel (ACS for every received
+    word) == table automaton (dense codes)."""
     z, meta = golden
     k, n, m, t1 = code_of(meta, name)
     t2 = code_of(meta, g2name)[3]
+    _three_explicit_paths_agree(pkg, k, n, m, t1, t2, N, p)
+
+
+# (23,35) m = 4 and (53,75) m = 5, delay-ordered taps: standard butterflies, the
+# k = 1 kernels at the intermediate memories
+_EXTRA_K1 = {4: ([[[1, 0, 0, 1, 1]], [[1, 1, 1, 0, 1]]], [[[1, 1, 1, 0, 1]], [[1, 0, 0, 1, 1]]]),
+             5: ([[[1, 0, 1, 0, 1, 1]], [[1, 1, 1, 1, 0, 1]]], [[[1, 1, 1, 1, 0, 1]], [[1, 0, 1, 0, 1, 1]]])}
+
+
+@pytest.mark.parametrize("m,N,p", [(4, 800, 0.05), (4, 300, 0.3), (5, 1100, 0.02), (5, 500, 0.12)])
+def test_k1_kernels_intermediate_memory(pkg, dev, m, N, p):
+    t1, t2 = _EXTRA_K1[m]
+    _three_explicit_paths_agree(pkg, 1, 2, m, t1, t2, N, p, learn_len=20000)
+
+
+def _three_explicit_paths_agree(pkg, k, n, m, t1, t2, N, p, learn_len=None):
     det = pkg.Detector(k, n, m, t1, device=0)
-    model = det.model(p, 20000 if m == 6 else None, 200, 1.0, 77)
-    a = det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=pkg.PATH_EXPLICIT, return_sums=True)
-    b = det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=pkg.PATH_EXPLICIT_GENERIC, return_sums=True)
-    assert np.array_equal(a["sums"], b["sums"])
-    assert a["counts"].cpu().tolist() == b["counts"].cpu().tolist()
-    if m < 6:
+    model = det.model(p, 20000 if m == 6 else learn_len, 200, 1.0, 77)
+    runs = {path: det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=path, return_sums=True)
+            for path in (pkg.PATH_EXPLICIT, pkg.PATH_EXPLICIT_ORBIT, pkg.PATH_EXPLICIT_GENERIC)}
+    a = runs[pkg.PATH_EXPLICIT]
+    for path in (pkg.PATH_EXPLICIT_ORBIT, pkg.PATH_EXPLICIT_GENERIC):
+        assert np.array_equal(a["sums"], runs[path]["sums"]), path
+        assert a["counts"].cpu().tolist() == runs[path]["counts"].cpu().tolist(), path
+    if m < 6 and model.info()["kind"] == 0:
         c = det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=pkg.PATH_TABLE, return_sums=True)
         assert np.array_equal(a["sums"], c["sums"])

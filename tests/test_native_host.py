@@ -25,7 +25,7 @@ def test_lib_exports_every_header_symbol(pkg):
     assert len(names) >= 15
     for name in names:
         assert hasattr(lib, name), f"libcvd.so does not export {name}"
-    assert lib.cvd_version() == 1
+    assert lib.cvd_version() == pkg._lib.ABI_VERSION == 2
     assert set(names) <= set(pkg._lib.EXPORTS), "python binding misses a header function"
 
 
@@ -140,3 +140,14 @@ def test_sparse_model_m6(pkg):
     # a visited row's entries are (C + 1) / (R_i + S), an unvisited row's 1 / S
     assert np.all(lp >= math.log(1.0 / (20000 + inf["S"])))
     assert inf["logp1_unseen"] == math.log(1.0 / inf["S"])
+
+
+@pytest.mark.parametrize("name,kernel", [("m6_133_171", 3), ("m3_demo", 3), ("m2_75", 2), ("r23_m4", 1)])
+def test_explicit_kernel_selection(pkg, golden, name, kernel):
+    """The explicit path's kernel: butterfly (k = 1, n = 2, standard butterflies,
+    m >= 3), else orbit (k = 1), else generic."""
+    z, meta = golden
+    k, n, m, taps = code_of(meta, name)
+    mod = pkg.Model(pkg.Code(taps, m, k, n), 0.05, 5000, 200, 1.0, 7, enum_cap=100)
+    assert mod.info()["explicit_kernel"] == kernel
+    assert kernel in pkg.KERNEL_NAMES
