@@ -361,16 +361,20 @@ extern "C" int cvd_enumerate(const cvd_code* dec, int64_t cap, int64_t* S_out, u
 namespace {
 
 void build_hash(cvd_model& Mo) {
-  // Explicit-path row table: an open-addressing directory over the
-  // nibble-packed metric vectors (fingerprints + keys) and, per slot, the row
-  // record {log P̂1[r], slot of successor(r) or -1}.  The successor slots let a
-  // sequence walk learned rows without hashing (table mode).
+  // Explicit-path row table: a Bloom filter over the row keys, and an
+  // open-addressing directory (linear probing) of the nibble-packed metric
+  // vectors with, per slot, the row record {log P̂1[r], slot of successor(r)
+  // or -1}.  The successor slots let a sequence walk learned rows without
+  // hashing (table mode); the filter ends most lookups of non-rows.
   const int m = Mo.dec.m, M = 1 << m, R = 1 << Mo.dec.n, nw = nib_words(m);
   int64_t cap = 64;
-  while (cap < 4 * Mo.n_rows) cap <<= 1;   // load factor <= 1/4: most misses end at the home slot
+  while (cap < 8 * Mo.n_rows) cap <<= 1;   // load factor <= 1/8: a hit is at its home slot ~94% of the time
   Mo.hcap = cap;
-  Mo.h_fp.assign((size_t)cap, 0u);
-  Mo.h_key.assign((size_t)cap * nw, 0u);
+  int64_t fcap = 64;
+  while (fcap * 4 < Mo.n_rows) fcap <<= 1;   // >= 16 filter bits per row
+  Mo.fcap = fcap;
+  Mo.h_filt.assign((size_t)fcap * 2, 0u);
+  Mo.h_key.assign((size_t)cap * nw, kEmptyKey);
   Mo.h_rsw = row_words(Mo.dec.n);
   Mo.h_row.assign((size_t)cap * Mo.h_rsw, 0u);
   Mo.max_probe = 0;
@@ -382,11 +386,14 @@ void build_hash(cvd_model& Mo) {
       for (int w = 0; w < nw; ++w) kw[w] = key_swap(kw[w]);   // device key layout
     uint32_t h1, h2;
     key_hash(kw.data(), nw, h1, h2);
+    uint32_t wi, lo, hi;
+    filter_probe(h1, h2, (uint32_t)(fcap - 1), wi, lo, hi);
+    Mo.h_filt[2 * (size_t)wi] |= lo;
+    Mo.h_filt[2 * (size_t)wi + 1] |= hi;
     uint64_t slot = h1 & (uint64_t)(cap - 1);
     int probe = 0;
-    while (Mo.h_fp[slot]) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
+    while (Mo.h_key[slot * nw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
     Mo.max_probe = std::max(Mo.max_probe, probe);
-    Mo.h_fp[slot] = h2 | 1u;
     for (int w = 0; w < nw; ++w) Mo.h_key[slot * nw + w] = kw[w];
     slot_of[(size_t)i] = (int64_t)slot;
   }

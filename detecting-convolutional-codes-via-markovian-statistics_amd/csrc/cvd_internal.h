@@ -30,8 +30,9 @@ struct cvd_model {
   int64_t hcap = 0;               // power of two, 0 = none
   int32_t max_probe = 0;
   std::vector<int64_t> row_next;  // [n_rows][2^n] row index of successor(row, r), -1 if not a row
-  std::vector<uint32_t> h_fp;     // [hcap] fingerprint | 1, 0 = empty
-  std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector
+  std::vector<uint32_t> h_filt;   // [fcap][2] blocked Bloom filter words (filter_probe)
+  int64_t fcap = 0;               // filter words, power of two
+  std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector, word 0 = kEmptyKey if empty
   int32_t h_rsw = 0;              // row record stride in dwords (row_words)
   std::vector<uint32_t> h_row;    // [hcap][h_rsw]: log P̂1[r] (2^n f64), successor slot[r] (2^n i32)
   int32_t slot0 = 0;              // slot of D_0 = 0
@@ -52,7 +53,7 @@ struct cvd_model {
   uint32_t* d_rec = nullptr;
   double* d_logp1 = nullptr;
   double* d_ltref = nullptr;
-  uint32_t* d_fp = nullptr;
+  uint32_t* d_filt = nullptr;
   uint32_t* d_hkey = nullptr;
   uint32_t* d_hrow = nullptr;
   uint32_t* d_bmp = nullptr;
@@ -64,8 +65,10 @@ namespace cvd {
 
 void set_error(const std::string& msg);
 inline int nib_words(int m) { return (1 << m) >= 8 ? (1 << m) / 8 : 1; }
-// row record: 2^n doubles + 2^n int32 successor slots, padded to 16 B
-CVD_HD int row_words(int n) { return (3 * (1 << n) + 3) & ~3; }
+// row record: 2^n doubles + 2^n int32 successor slots, padded to a power of
+// two (64 B at n = 2: one record never straddles a cache line)
+constexpr int row_words_c(int R) { return 3 * R <= 4 ? 4 : 2 * row_words_c((R + 1) / 2); }
+CVD_HD int row_words(int n) { return row_words_c(1 << n); }
 
 // Nibble packing of a metric vector: state s in nibble s (word s / 8, bits 4*(s % 8)).
 void pack_nibbles(const uint8_t* D, int M, uint32_t* out);
@@ -95,6 +98,21 @@ CVD_HD void key_hash(const uint32_t* w, int nw, uint32_t& h1, uint32_t& h2) {
   uint32_t b = (h ^ (h >> 13)) * 0xC2B2AE35u;
   h2 = b ^ (b >> 15);
 }
+
+// Blocked Bloom filter over the row keys (explicit path): one 64-bit word per
+// key, two bits in each 32-bit half.  A lookup of a state that is not a row
+// (most lookups at p >= 0.05 and for every H2 sequence) ends on this one
+// L2-resident load.  Word index from h2, bit positions from a third mix.
+CVD_HD void filter_probe(uint32_t h1, uint32_t h2, uint32_t fmask, uint32_t& wi, uint32_t& lo,
+                         uint32_t& hi) {
+  wi = h2 & fmask;
+  const uint32_t h3 = (h1 ^ rotl32(h2, 16)) * 0x9E3779B1u;
+  lo = (1u << (h3 >> 27)) | (1u << ((h3 >> 22) & 31u));
+  hi = (1u << ((h3 >> 17) & 31u)) | (1u << ((h3 >> 12) & 31u));
+}
+// empty hash slot: key word 0 (a nibble-packed metric vector never has 15 in
+// every nibble, metrics stay <= (ceil(m/k)+1) n - 1 <= 14)
+constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;
 
 // kernel launchers (cvd_kernels.hip)
 int launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, uint64_t thr,

@@ -247,14 +247,14 @@ __global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
 // ────────────────────────── explicit metric path ────────────────────────────
 
 struct ExpArgs {
-  const uint32_t* fp;       // [hcap] fingerprint | 1, 0 = empty
-  const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors
+  const uint32_t* filt;     // [fmask + 1][2] Bloom filter words over the row keys (filter_probe)
+  const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors, word 0 = kEmptyKey if empty
   const uint32_t* hrow;     // [hcap][row_words(n)]: log P̂1[r] (f64), successor slot[r] (i32, -1 = not a row)
   const double* ltref;      // [R + 1]
   const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
   uint32_t bfly_uni;        // k = 1 butterfly kernel: every out(j, 0), j < 2^(m-1), in one class
-  uint32_t hmask;
+  uint32_t hmask, fmask;
   int32_t max_probe;
   int32_t slot0;            // slot of D_0 = 0
   double lp_unseen;
@@ -300,15 +300,19 @@ struct StreamReader {
 // slot of its successor for every received word, so a sequence that stays in
 // learned states walks rows with one small prefetched load per step and no
 // hashing ("table mode").  After an unvisited state the successor is unknown
-// and the next state is hashed: its fingerprint is fetched one step ahead, the
-// key and row entries only on a fingerprint match (mid-step), and the exact
-// key compare happens when the step resolves.  slot: >= 0 known row,
-// -1 known unvisited row, -2 pending hash probe (hs, fpv, pf).
+// and the next state is hashed: its Bloom-filter word is fetched one step
+// ahead (L2-resident; a negative answer -- almost every non-row -- ends the
+// lookup), the key and row entries of the home slot only on a positive answer
+// (mid-step), and the exact key compare, with linear probing past an occupied
+// home slot, happens when the step resolves.  slot: >= 0 known row, -1 known
+// unvisited row, -2 pending hash probe (hs, filter word fw, bits flo/fhi).
 template <int NW, int R>
 struct RowCursor {
-  static constexpr int RSW = (3 * R + 3) & ~3;
+  static constexpr int RSW = row_words_c(R);
   int32_t slot, pnx;
-  uint32_t hs, fpv, pf;
+  uint32_t hs, flo, fhi;
+  uint2 fw;
+  bool cand;
   double plp;
   uint32_t pkey[NW];
   __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
@@ -317,11 +321,12 @@ struct RowCursor {
     pnx = (int32_t)rw[2 * R + rn];
   }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
-    slot = a.slot0; pf = 0u; hs = 0u; fpv = 0u;
+    slot = a.slot0; hs = 0u; flo = fhi = 0u; fw = make_uint2(0u, 0u); cand = false;
     prefetch_row(a, slot, r0);
   }
   __device__ void mid(const ExpArgs& a, uint32_t r) {
-    if (slot == -2 && pf == fpv) {
+    cand = slot == -2 && (fw.x & flo) == flo && (fw.y & fhi) == fhi;
+    if (cand) {
       const uint32_t* k = a.hkey + (size_t)hs * NW;
 #pragma unroll
       for (int w = 0; w < NW; ++w) pkey[w] = k[w];
@@ -334,29 +339,27 @@ struct RowCursor {
     int32_t ns = -2;
     if (slot >= 0) {
       lpv = plp; ns = pnx;
-    } else if (slot == -2 && pf != 0u) {
-      bool eq = pf == fpv;
+    } else if (cand) {
+      bool eq = true;
 #pragma unroll
       for (int w = 0; w < NW; ++w) eq = eq && (pkey[w] == key[w]);
       if (eq) {
         lpv = plp; ns = pnx;
-      } else {
+      } else if (pkey[0] != kEmptyKey) {
+        // home slot holds another row: linear probing up to an empty slot
         uint32_t sl = hs;
         for (int pr = 1; pr <= a.max_probe; ++pr) {
           sl = (sl + 1u) & a.hmask;
-          const uint32_t f = a.fp[sl];
-          if (f == 0u) break;
-          if (f == fpv) {
-            const uint32_t* k = a.hkey + (size_t)sl * NW;
-            bool e2 = true;
+          const uint32_t* k = a.hkey + (size_t)sl * NW;
+          if (k[0] == kEmptyKey) break;
+          bool e2 = true;
 #pragma unroll
-            for (int w = 0; w < NW; ++w) e2 = e2 && (k[w] == key[w]);
-            if (e2) {
-              const uint32_t* rw = a.hrow + (size_t)sl * RSW;
-              lpv = reinterpret_cast<const double*>(rw)[r];
-              ns = (int32_t)rw[2 * R + r];
-              break;
-            }
+          for (int w = 0; w < NW; ++w) e2 = e2 && (k[w] == key[w]);
+          if (e2) {
+            const uint32_t* rw = a.hrow + (size_t)sl * RSW;
+            lpv = reinterpret_cast<const double*>(rw)[r];
+            ns = (int32_t)rw[2 * R + r];
+            break;
           }
         }
       }
@@ -369,11 +372,11 @@ struct RowCursor {
     if (slot >= 0) {
       prefetch_row(a, slot, rn);
     } else if (slot == -2) {
-      uint32_t h1, h2;
+      uint32_t h1, h2, wi;
       key_hash(key, NW, h1, h2);
       hs = h1 & a.hmask;
-      fpv = h2 | 1u;
-      pf = a.fp[hs];
+      filter_probe(h1, h2, a.fmask, wi, flo, fhi);
+      fw = reinterpret_cast<const uint2*>(a.filt)[wi];
     }
   }
 };
@@ -743,14 +746,27 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
                                         uint32_t sel, uint32_t O8, uint32_t& zn) {
   constexpr int M = 1 << m, H = M / 2;
   uint32_t E[H];
+#ifdef CVD_ABL_SPEC
+  const uint32_t e0 = __builtin_popcount(rr), e1 = __builtin_popcount(rr ^ 1u);
+  const uint32_t W0 = e0 | ((2u - e0) << 16), W1 = e1 | ((2u - e1) << 16);
+#endif
 #pragma unroll
   for (int j = 0; j < H; ++j) {
+#ifndef CVD_ABL_NOCURSOR
     if (j == H / 2) cur.mid(a, rr);     // fingerprint matched: key + row loads under the second half
-    const uint32_t T = tb[j];
+#endif
     const us2 pa = as_us2(Dp[j >> 1]), pb = as_us2(Dp[(j >> 1) + H / 2]);
     const us2 da = (j & 1) ? __builtin_shufflevector(pa, pa, 1, 1) : __builtin_shufflevector(pa, pa, 0, 0);
     const us2 db = (j & 1) ? __builtin_shufflevector(pb, pb, 1, 1) : __builtin_shufflevector(pb, pb, 0, 0);
+#ifdef CVD_ABL_SPEC
+    const int xj = (int)((CVD_ABL_SPEC >> (2 * j)) & 3u);
+    const us2 W = xj == 0 ? as_us2(W0) : xj == 1 ? as_us2(W1) : xj == 2 ? __builtin_shufflevector(as_us2(W1), as_us2(W1), 1, 0)
+                                                                          : __builtin_shufflevector(as_us2(W0), as_us2(W0), 1, 0);
+    (void)tb;
+#else
+    const uint32_t T = tb[j];
     const us2 W = as_us2(__builtin_amdgcn_perm(T, T, sel));   // (e, 2 - e)
+#endif
     E[j] = as_u32(__builtin_elementwise_min(da + W, db + __builtin_shufflevector(W, W, 1, 0)));
     if ((j & 3) == 3) {
       // word w = states 8w..8w+7 in nibble order bitrev3 (device key layout)
@@ -811,7 +827,11 @@ __global__ __launch_bounds__(kBlock, kK1bWavesPerSimd) void detect_k1b_kernel(Ex
       O += mu;
       O8 += mu8;
       // P̂1 row of D_{t-1}
+#ifdef CVD_ABL_NOCURSOR
+      lp += (double)(key[0] & 7u);
+#else
       lp += cur.resolve(a, key, rr);          // Pd_plotter.py:115, T = P̂1
+#endif
       uint32_t sym = 0u;
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
@@ -822,7 +842,9 @@ __global__ __launch_bounds__(kBlock, kK1bWavesPerSimd) void detect_k1b_kernel(Ex
       const uint32_t c = 1u + ((sym & 0xFFFFu) == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
       lr += s_lt[c];                          // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
       if (a.trace) write_trace<m, 1, 2, true>(a.trace, t, a.nseq, q, key);
+#ifndef CVD_ABL_NOCURSOR
       cur.prefetch(a, key, rn);
+#endif
       rd.advance();
       if ((t & (kRenorm - 1)) == 0) {
         const us2 o2 = as_us2(O * 0x10001u);
@@ -956,13 +978,13 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   ExpKernel kern = nullptr;
   const uint32_t* bmp = nullptr;
   select_explicit(M, variant, &kern, &bmp);
-  if (!kern || !M.d_fp || !bmp) { set_error("explicit path: unsupported code shape (m,k,n)"); return CVD_E_UNSUPPORTED; }
+  if (!kern || !M.d_filt || !bmp) { set_error("explicit path: unsupported code shape (m,k,n)"); return CVD_E_UNSUPPORTED; }
   if (nseq <= 0) return CVD_OK;
   ExpArgs a;
-  a.fp = M.d_fp; a.hkey = M.d_hkey; a.hrow = M.d_hrow; a.ltref = M.d_ltref;
+  a.filt = M.d_filt; a.hkey = M.d_hkey; a.hrow = M.d_hrow; a.ltref = M.d_ltref;
   a.bmp = bmp; a.slot0 = M.slot0;
   a.repmap = M.repmap; a.swmap = M.swmap; a.bfly_uni = M.bfly_uni;
-  a.hmask = (uint32_t)(M.hcap - 1); a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
+  a.hmask = (uint32_t)(M.hcap - 1); a.fmask = (uint32_t)(M.fcap - 1); a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   a.trace = d_trace;
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
@@ -982,7 +1004,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_logp1, M.logp1))) return rc;
   }
   if (M.hcap > 0) {
-    if ((rc = dev_copy(M.d_fp, M.h_fp))) return rc;
+    if ((rc = dev_copy(M.d_filt, M.h_filt))) return rc;
     if ((rc = dev_copy(M.d_hkey, M.h_key))) return rc;
     if ((rc = dev_copy(M.d_hrow, M.h_row))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
@@ -998,11 +1020,11 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_fp, M.d_hkey, M.d_hrow, M.d_bmp, M.d_bmk1, M.d_bfly};
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_hkey, M.d_hrow, M.d_bmp, M.d_bmk1, M.d_bfly};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
-  M.d_fp = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
+  M.d_filt = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
   M.d_bfly = nullptr;
   M.device = -1;
   (void)hipSetDevice(cur);
