@@ -8,6 +8,7 @@
 #include <cstring>
 #include <memory>
 #include <new>
+#include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -369,6 +370,9 @@ void build_hash(cvd_model& Mo) {
   const int m = Mo.dec.m, M = 1 << m, R = 1 << Mo.dec.n, nw = nib_words(m);
   int64_t cap = 64;
   while (cap < 8 * Mo.n_rows) cap <<= 1;   // load factor <= 1/8: a hit is at its home slot ~94% of the time
+  // device offsets are 32-bit byte offsets into the row records
+  if (cap * (int64_t)row_words(Mo.dec.n) * 4 > ((int64_t)1 << 32))
+    throw std::length_error("explicit-path row table over 4 GiB (too many learned rows)");
   Mo.hcap = cap;
   int64_t fcap = 64;
   while (fcap * 4 < Mo.n_rows) fcap <<= 1;   // >= 16 filter bits per row
@@ -451,11 +455,14 @@ void build_bfly(cvd_model& Mo, const Tabs& T) {
   }
   Mo.bfly.assign((size_t)H, 0u);
   Mo.bfly_uni = 1u;
+  for (uint32_t& w : Mo.bfly_even) w = 0u;
   for (int j = 0; j < H; ++j) {
     const uint32_t x = T.out[j * T.K + 0];
     for (uint32_t y = 0; y < 4; ++y) Mo.bfly[(size_t)j] |= (uint32_t)__builtin_popcount(x ^ y) << (8 * y);
     // class of out(j, 0): {00, 11} or {01, 10}; out(0, 0) = 00
     if (__builtin_popcount(x) & 1) Mo.bfly_uni = 0u;
+    // nibble of state j in the halves-difference words (device key layout)
+    else Mo.bfly_even[j / 8] |= 0xFu << (4 * key_nibble(T.M, j));
   }
   Mo.k1b_ok = true;
 }

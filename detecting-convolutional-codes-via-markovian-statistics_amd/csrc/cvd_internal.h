@@ -46,6 +46,7 @@ struct cvd_model {
   // both 11): per butterfly j, byte y of bfly[j] = popcount(out(j, 0) ^ y)
   bool k1b_ok = false;
   uint32_t bfly_uni = 0;           // every out(j, 0), j < 2^(m-1), in {00, 11}
+  uint32_t bfly_even[4] = {0, 0, 0, 0};   // nibble masks of the butterflies j with out(j, 0) in {00, 11}
   std::vector<uint32_t> bfly;      // [2^m / 2]
 
   // device copies

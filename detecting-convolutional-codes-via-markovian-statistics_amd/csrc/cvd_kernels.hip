@@ -254,6 +254,7 @@ struct ExpArgs {
   const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
   uint32_t bfly_uni;        // k = 1 butterfly kernel: every out(j, 0), j < 2^(m-1), in one class
+  uint32_t bfly_even[4];    // k = 1 butterfly kernel: nibble masks of the butterflies with out(j, 0) in {00, 11}
   uint32_t hmask, fmask;
   int32_t max_probe;
   int32_t slot0;            // slot of D_0 = 0
@@ -306,9 +307,16 @@ struct StreamReader {
 // (mid-step), and the exact key compare, with linear probing past an occupied
 // home slot, happens when the step resolves.  slot: >= 0 known row, -1 known
 // unvisited row, -2 pending hash probe (hs, filter word fw, bits flo/fhi).
+// 32-bit byte offsets from a uniform base (global_load with an SGPR base: no
+// 64-bit address arithmetic per lane)
+template <typename T>
+__device__ __forceinline__ T ld_off(const void* base, uint32_t byte_off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 template <int NW, int R>
 struct RowCursor {
-  static constexpr int RSW = row_words_c(R);
+  static constexpr uint32_t RSB = 4u * row_words_c(R);   // record bytes
   int32_t slot, pnx;
   uint32_t hs, flo, fhi;
   uint2 fw;
@@ -316,9 +324,9 @@ struct RowCursor {
   double plp;
   uint32_t pkey[NW];
   __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
-    const uint32_t* rw = a.hrow + (size_t)s * RSW;
-    plp = reinterpret_cast<const double*>(rw)[rn];
-    pnx = (int32_t)rw[2 * R + rn];
+    const uint32_t off = (uint32_t)s * RSB;
+    plp = ld_off<double>(a.hrow, off + 8u * rn);
+    pnx = ld_off<int32_t>(a.hrow, off + 4u * (2u * R + rn));
   }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
     slot = a.slot0; hs = 0u; flo = fhi = 0u; fw = make_uint2(0u, 0u); cand = false;
@@ -327,11 +335,19 @@ struct RowCursor {
   __device__ void mid(const ExpArgs& a, uint32_t r) {
     cand = slot == -2 && (fw.x & flo) == flo && (fw.y & fhi) == fhi;
     if (cand) {
-      const uint32_t* k = a.hkey + (size_t)hs * NW;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) pkey[w] = k[w];
+      for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs * NW + w) * 4u);
       prefetch_row(a, (int32_t)hs, r);
     }
+  }
+  __device__ static bool same_key(const uint32_t (&x)[NW], const uint32_t (&y)[NW]) {
+    uint32_t d = 0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) d |= x[w] ^ y[w];
+    // keep the xor/or reduction (2-cycle VALU); without the asm LLVM rewrites it
+    // into per-word compares materialised through v_cndmask
+    asm volatile("" : "+v"(d));
+    return d == 0u;
   }
   // log P̂1(row(D_{t-1}), r); afterwards `slot` describes row(D_t)
   __device__ double resolve(const ExpArgs& a, const uint32_t (&key)[NW], uint32_t r) {
@@ -340,27 +356,23 @@ struct RowCursor {
     if (slot >= 0) {
       lpv = plp; ns = pnx;
     } else if (cand) {
-      bool eq = true;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) eq = eq && (pkey[w] == key[w]);
-      if (eq) {
+      if (same_key(pkey, key)) {
         lpv = plp; ns = pnx;
       } else if (pkey[0] != kEmptyKey) {
         // home slot holds another row: linear probing up to an empty slot
         uint32_t sl = hs;
+        bool found = false;
         for (int pr = 1; pr <= a.max_probe; ++pr) {
           sl = (sl + 1u) & a.hmask;
-          const uint32_t* k = a.hkey + (size_t)sl * NW;
-          if (k[0] == kEmptyKey) break;
-          bool e2 = true;
+          uint32_t k[NW];
 #pragma unroll
-          for (int w = 0; w < NW; ++w) e2 = e2 && (k[w] == key[w]);
-          if (e2) {
-            const uint32_t* rw = a.hrow + (size_t)sl * RSW;
-            lpv = reinterpret_cast<const double*>(rw)[r];
-            ns = (int32_t)rw[2 * R + r];
-            break;
-          }
+          for (int w = 0; w < NW; ++w) k[w] = ld_off<uint32_t>(a.hkey, (sl * NW + w) * 4u);
+          if (k[0] == kEmptyKey) break;
+          if (same_key(k, key)) { found = true; break; }
+        }
+        if (found) {
+          lpv = ld_off<double>(a.hrow, sl * RSB + 8u * r);
+          ns = ld_off<int32_t>(a.hrow, sl * RSB + 4u * (2u * R + r));
         }
       }
     }
@@ -376,7 +388,10 @@ struct RowCursor {
       key_hash(key, NW, h1, h2);
       hs = h1 & a.hmask;
       filter_probe(h1, h2, a.fmask, wi, flo, fhi);
-      fw = reinterpret_cast<const uint2*>(a.filt)[wi];
+      // one 8-byte load into both halves (two dword loads into two fields would
+      // be sunk with prefetch_row's stores behind a pointer phi: scratch)
+      const uint64_t f = ld_off<uint64_t>(a.filt, wi * 8u);
+      fw = make_uint2((uint32_t)f, (uint32_t)(f >> 32));
     }
   }
 };
@@ -769,9 +784,10 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
 #endif
     E[j] = as_u32(__builtin_elementwise_min(da + W, db + __builtin_shufflevector(W, W, 1, 0)));
     if ((j & 3) == 3) {
-      // word w = states 8w..8w+7 in nibble order bitrev3 (device key layout)
-      const uint32_t x = E[j - 3] + (E[j - 2] << 8);
-      const uint32_t y = E[j - 1] + (E[j] << 8);
+      // word w = states 8w..8w+7 in nibble order bitrev3 (device key layout):
+      // bytes (E0.lo, E1.lo, E0.hi, E1.hi) by one v_perm (metrics + O < 256)
+      const uint32_t x = __builtin_amdgcn_perm(E[j - 2], E[j - 3], 0x06020400u);
+      const uint32_t y = __builtin_amdgcn_perm(E[j], E[j - 1], 0x06020400u);
       const uint32_t v = x + (y << 4) - O8;             // nibbles = raw metric - offset <= 14
       zn |= (v - 0x11111111u) & ~v;
       kw[j >> 2] = v;
@@ -807,14 +823,26 @@ __global__ __launch_bounds__(kBlock, kK1bWavesPerSimd) void detect_k1b_kernel(Ex
     for (int64_t t = 1; t <= a.N; ++t) {
       const uint32_t rr = rd.peek();
       const uint32_t rn = t < a.N ? rd.peek_next() : 0u;
-      // halves test: D_{t-1}(j) == D_{t-1}(j + 2^(m-1)) for every j
-      uint32_t hx = 0u;
+      // halves differences of D_{t-1}: nibble of state j (< 2^(m-1)) is nonzero
+      // iff D_{t-1}(j) != D_{t-1}(j + 2^(m-1))
+      constexpr int NH = NW >= 2 ? NW / 2 : 1;
+      uint32_t dh[NH];
       if constexpr (NW >= 2) {
 #pragma unroll
-        for (int w = 0; w < NW / 2; ++w) hx |= key[w] ^ key[w + NW / 2];
+        for (int w = 0; w < NH; ++w) dh[w] = key[w] ^ key[w + NH];
       } else {
-        hx = (key[0] ^ (key[0] >> 4)) & 0x0F0F0F0Fu;   // states s, s + 4 = nibbles 2i, 2i + 1
+        dh[0] = (key[0] ^ (key[0] >> 4)) & 0x0F0F0F0Fu;   // states s, s + 4 = nibbles 2i, 2i + 1
       }
+      uint32_t hx = 0u, se = 0u, so = 0u;
+#pragma unroll
+      for (int w = 0; w < NH; ++w) {
+        hx |= dh[w];
+        se |= dh[w] & a.bfly_even[w];
+        so |= dh[w] & ~a.bfly_even[w];
+      }
+      // D_t(y) == its pair swap iff D_{t-1}(j) == D_{t-1}(j + 2^(m-1)) for every
+      // butterfly with e_j in {0, 2}, i.e. out(j, 0) in the class of y
+      const uint32_t sym = (__builtin_popcount(rr) & 1u) ? so : se;
       const uint32_t sel = rr | ((rr ^ 3u) << 16) | 0x0C000C00u;
       cu32* tb = as_const(a.bmp);
       asm volatile("" : "+s"(tb));   // per step: the table is re-read (scalar cache), not held in SGPRs
@@ -832,14 +860,10 @@ __global__ __launch_bounds__(kBlock, kK1bWavesPerSimd) void detect_k1b_kernel(Ex
 #else
       lp += cur.resolve(a, key, rr);          // Pd_plotter.py:115, T = P̂1
 #endif
-      uint32_t sym = 0u;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        key[w] = kw[w] - mu8;
-        sym |= key[w] ^ (key[w] >> 16);        // pairs (2j, 2j+1) = nibbles i, i + 4
-      }
+      for (int w = 0; w < NW; ++w) key[w] = kw[w] - mu8;
       // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni
-      const uint32_t c = 1u + ((sym & 0xFFFFu) == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
+      const uint32_t c = 1u + (sym == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
       lr += s_lt[c];                          // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
       if (a.trace) write_trace<m, 1, 2, true>(a.trace, t, a.nseq, q, key);
 #ifndef CVD_ABL_NOCURSOR
@@ -984,6 +1008,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   a.filt = M.d_filt; a.hkey = M.d_hkey; a.hrow = M.d_hrow; a.ltref = M.d_ltref;
   a.bmp = bmp; a.slot0 = M.slot0;
   a.repmap = M.repmap; a.swmap = M.swmap; a.bfly_uni = M.bfly_uni;
+  for (int w = 0; w < 4; ++w) a.bfly_even[w] = M.bfly_even[w];
   a.hmask = (uint32_t)(M.hcap - 1); a.fmask = (uint32_t)(M.fcap - 1); a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   a.trace = d_trace;
