@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--learn-len", type=int, default=1_000_000,
                     help="P̂1 learning chain length for non-enumerable codes")
     ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--p", type=float, default=None, help="diagnostic: run one p instead of the sweep")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle port (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "detector_pmc.json"),
@@ -73,6 +74,8 @@ def main():
     k, n, m = cc["k"], cc["n"], cc["m"]
     N = a.N if a.N is not None else {"m6": 100_000, "m2": 10_000, "r23_m4": 100_000}[a.config]
     p_grid = P_GRID if a.config != "m2" else [0.05]
+    if a.p is not None:
+        p_grid = [a.p]   # diagnostic: one grid point only (not the headline sweep)
     det = pkg.Detector(k, n, m, cc["gen1"], device=local)
     g1 = pkg.Code(cc["gen1"], m, k, n)
     g2 = pkg.Code(cc["gen2"], m, k, n)
@@ -172,6 +175,7 @@ def main():
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
                        "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
                        "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
+                       "detector_ms_steps": det_each,
                        "per_p": per_p},
     }
     if a.cpu_baseline and world == 1:

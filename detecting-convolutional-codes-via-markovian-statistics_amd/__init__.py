@@ -4,7 +4,7 @@ Drop-in for the hot path of So-bonkers/Detecting-Convolutional-Codes-Via-Markovi
 (Pd_plotter.run_experiment and the functions beneath it), running on gfx950
 through libcvd.so (include/cvd.h).  See DESIGN.md.
 """
-from ._lib import CvdError, lib, PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, KERNEL_NAMES  # noqa: F401
+from ._lib import CvdError, lib, PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY, KERNEL_NAMES  # noqa: F401
 from .codes import Code, EXAMPLE_CODES, CONFIG_CODES, octal_to_taps  # noqa: F401
 from .detector import (  # noqa: F401
     DEFAULTS, N_SPECTRUM_BY_M, Detector, Model, run_experiment, learn_P1_empirical,

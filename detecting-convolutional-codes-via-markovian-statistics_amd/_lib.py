@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
 ABI_VERSION = 2
 
-PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT = 0, 1, 2, 3, 4
+PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5
 
 
 class CvdError(RuntimeError):
@@ -44,7 +44,8 @@ class cvd_model_info(ctypes.Structure):
 
 KERNEL_NAMES = {0: "none", 1: "detect_explicit_kernel (generic explicit path)",
                 2: "detect_k1_kernel (k=1 orbit explicit path)",
-                3: "detect_k1b_kernel (k=1 butterfly explicit path)"}
+                3: "detect_k1b_kernel (k=1 butterfly explicit path, table-driven)",
+                4: "cvd_k1b_spec (k=1 butterfly explicit path, code-specialised at model upload)"}
 
 
 EXPORTS = {

@@ -1,0 +1,445 @@
+// Device code of the explicit path shared by the compiled kernels
+// (cvd_kernels.hip) and the code-specialised butterfly kernels hipRTC builds at
+// run time (cvd_rtc.cpp embeds this file and cvd_keys.h as source text): the
+// launch arguments, the received-word reader, the P̂1 row cursor and the k = 1,
+// n = 2 butterfly detector.  Self-contained: no standard-library includes.
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#else
+// hipRTC keeps its fixed-width types in __hip_internal
+typedef unsigned char uint8_t;
+typedef int int32_t;
+typedef unsigned int uint32_t;
+typedef long long int64_t;
+typedef unsigned long long uint64_t;
+typedef __SIZE_TYPE__ size_t;
+#endif
+#include "cvd_keys.h"
+
+namespace cvd_dev {
+
+using cvd::kEmptyKey;
+using cvd::row_words_c;
+using cvd::key_hash;
+using cvd::filter_probe;
+
+constexpr int kBlock = 256;
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// Uniform read-only tables go through the constant address space so that
+// uniform-index loads become scalar (s_load) loads into SGPRs instead of
+// per-lane vector loads the compiler would otherwise have to wait on.
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+__device__ __forceinline__ cu32* as_const(const uint32_t* p) { return (cu32*)p; }
+
+__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
+// (a << 4) | b as one v_lshl_or_b32 (the compiler otherwise splits nibble packs
+// into shifts + v_or3)
+__device__ __forceinline__ uint32_t lshl4_or(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// Received-word layout in HBM (include/cvd.h): words are grouped in 16-byte
+// chunks per sequence; word w of sequence q lives at
+// r[((w >> 2) * pitch + q) * 4 + (w & 3)], so each lane moves 16 B per load
+// and a wave reads / writes 1 KiB contiguously.
+__device__ __forceinline__ size_t chunk_index(int64_t w4, int64_t pitch, int64_t q) {
+  return ((size_t)w4 * (size_t)pitch + (size_t)q) * 4;
+}
+__device__ __forceinline__ uint32_t next_word(const uint32_t* r, int64_t pitch, int64_t q, int64_t w,
+                                              uint4& cache) {
+  if ((w & 3) == 0) cache = *reinterpret_cast<const uint4*>(r + chunk_index(w >> 2, pitch, q));
+  const int e = (int)(w & 3);
+  return e == 0 ? cache.x : e == 1 ? cache.y : e == 2 ? cache.z : cache.w;
+}
+
+// Lane index in the wave (v_mbcnt; cheap to recompute instead of keeping live:
+// the laundered mask keeps LLVM from merging two calls and holding the first
+// result across the step loop).
+__device__ __forceinline__ uint32_t lane_id() {
+  uint32_t all = ~0u;
+  asm volatile("" : "+s"(all));
+  return __builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+}
+
+// count_decisions with validity and hypothesis given as wave ballots.
+__device__ __forceinline__ void count_decisions_masked(uint64_t vmask, uint64_t hmask, double lp, double lr,
+                                                       int64_t* counts) {
+  const uint64_t gt = __ballot(lp > lr), le = __ballot(lp <= lr);
+  const uint64_t b1 = gt & vmask & hmask;     // Pd_plotter.py:215
+  const uint64_t b2 = le & vmask & ~hmask;    // Pd_plotter.py:222
+  if (lane_id() == 0) {
+    if (b1) atomicAdd(reinterpret_cast<unsigned long long*>(counts), (unsigned long long)__popcll(b1));
+    if (b2) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), (unsigned long long)__popcll(b2));
+  }
+}
+
+// Wave-level success counting: one 64-bit atomic per wave and hypothesis.
+__device__ __forceinline__ void count_decisions(bool valid, bool is_h1, double lp, double lr,
+                                                int64_t* counts) {
+  const bool s1 = valid && is_h1 && (lp > lr);     // Pd_plotter.py:215
+  const bool s2 = valid && !is_h1 && (lp <= lr);   // Pd_plotter.py:222
+  const unsigned long long b1 = __ballot(s1), b2 = __ballot(s2);
+  if ((threadIdx.x & 63) == 0) {
+    if (b1) atomicAdd(reinterpret_cast<unsigned long long*>(counts), (unsigned long long)__popcll(b1));
+    if (b2) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), (unsigned long long)__popcll(b2));
+  }
+}
+
+// ────────────────────────── explicit metric path ────────────────────────────
+
+struct ExpArgs {
+  const uint32_t* filt;     // [fmask + 1][2] Bloom filter words over the row keys (filter_probe)
+  const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors, word 0 = kEmptyKey if empty
+  const uint32_t* hrow;     // [hcap][row_words(n)]: log P̂1[r] (f64), successor slot[r] (i32, -1 = not a row)
+  const double* ltref;      // [R + 1]
+  const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
+  uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
+  uint32_t bfly_uni;        // k = 1 butterfly kernel: every out(j, 0), j < 2^(m-1), in one class
+  uint32_t bfly_even[4];    // k = 1 butterfly kernel: nibble masks of the butterflies with out(j, 0) in {00, 11}
+  uint32_t hmask, fmask;
+  int32_t max_probe;
+  int32_t slot0;            // slot of D_0 = 0
+  double lp_unseen;
+  int64_t N, nseq, n_h1;
+  const uint32_t* r;
+  double* sums;
+  int64_t* counts;
+  uint8_t* trace;
+};
+
+// Received words of one sequence, one word of lookahead (the next step's r is
+// known before the current step ends, so its P̂1 row entry can be prefetched).
+template <int n>
+struct StreamReader {
+  static constexpr int SPW = 32 / n;
+  static constexpr uint32_t MASK = (1u << n) - 1u;
+  const uint32_t* r;
+  int64_t pitch, q, N, nwords, wi;
+  uint4 cache;
+  uint32_t cur, nxt;
+  int left;
+  __device__ int steps_in(int64_t w) const { return (int)min((int64_t)SPW, N - w * SPW); }
+  __device__ void init(const uint32_t* r_, int64_t pitch_, int64_t q_, int64_t N_) {
+    r = r_; pitch = pitch_; q = q_; N = N_;
+    nwords = (N + SPW - 1) / SPW;
+    cur = nxt = 0u; left = 0; wi = 0;
+    if (nwords > 0) { cur = next_word(r, pitch, q, 0, cache); left = steps_in(0); }
+    wi = 1;
+    if (wi < nwords) nxt = next_word(r, pitch, q, wi, cache);
+  }
+  __device__ uint32_t peek() const { return cur & MASK; }
+  __device__ uint32_t peek_next() const { return left > 1 ? ((cur >> n) & MASK) : (nxt & MASK); }
+  __device__ void advance() {
+    if (left > 1) { cur >>= n; --left; return; }
+    cur = nxt;
+    left = wi < nwords ? steps_in(wi) : 0;
+    ++wi;
+    if (wi < nwords) nxt = next_word(r, pitch, q, wi, cache);
+  }
+};
+
+// Lookup of the P̂1 row of the current metric state.  A learned row stores the
+// slot of its successor for every received word, so a sequence that stays in
+// learned states walks rows with one small prefetched load per step and no
+// hashing ("table mode").  After an unvisited state the successor is unknown
+// and the next state is hashed: its Bloom-filter word is fetched one step
+// ahead (L2-resident; a negative answer -- almost every non-row -- ends the
+// lookup), the key and row entries of the home slot only on a positive answer
+// (mid-step), and the exact key compare, with linear probing past an occupied
+// home slot, happens when the step resolves.  slot: >= 0 known row, -1 known
+// unvisited row, -2 pending hash probe (hs, filter word fw, bits flo/fhi).
+// 32-bit byte offsets from a uniform base (global_load with an SGPR base: no
+// 64-bit address arithmetic per lane)
+template <typename T>
+__device__ __forceinline__ T ld_off(const void* base, uint32_t byte_off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
+template <int NW, int R>
+struct RowCursor {
+  static constexpr uint32_t RSB = 4u * row_words_c(R);   // record bytes
+  int32_t slot, pnx;
+  uint32_t hs, flo, fhi;
+  uint2 fw;
+  bool cand;
+  double plp;
+  uint32_t pkey[NW];
+  __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
+    const uint32_t off = (uint32_t)s * RSB;
+    plp = ld_off<double>(a.hrow, off + 8u * rn);
+    pnx = ld_off<int32_t>(a.hrow, off + 4u * (2u * R + rn));
+  }
+  __device__ void start(const ExpArgs& a, uint32_t r0) {
+    slot = a.slot0; hs = 0u; flo = fhi = 0u; fw = make_uint2(0u, 0u); cand = false;
+    prefetch_row(a, slot, r0);
+  }
+  // Ordering fences: nothing in mid() / resolve() depends on the ACS, so
+  // without these LLVM hoists both to the top of the step, where the loads
+  // issued one step (filter word, row) or half a step (key, row) earlier are
+  // waited for at once.  Each fence makes the cursor state an output of an asm
+  // that consumes an ACS result (the running zero-nibble test, which depends on
+  // every butterfly computed so far), so the waits land after that much work.
+  __device__ void fence(uint32_t dep) {
+    asm volatile("" : "+v"(fw.x), "+v"(fw.y), "+v"(slot), "+v"(pnx), "+v"(plp) : "v"(dep));
+  }
+  template <int N_>
+  __device__ void fence_keys(uint32_t dep) {
+#pragma unroll
+    for (int w = 0; w < N_; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
+  }
+  __device__ void mid(const ExpArgs& a, uint32_t r) {
+    cand = slot == -2 && (fw.x & flo) == flo && (fw.y & fhi) == fhi;
+    if (cand) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs * NW + w) * 4u);
+      prefetch_row(a, (int32_t)hs, r);
+    }
+  }
+  __device__ static bool same_key(const uint32_t (&x)[NW], const uint32_t (&y)[NW]) {
+    uint32_t d = 0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) d |= x[w] ^ y[w];
+    // keep the xor/or reduction (2-cycle VALU); without the asm LLVM rewrites it
+    // into per-word compares materialised through v_cndmask
+    asm volatile("" : "+v"(d));
+    return d == 0u;
+  }
+  // log P̂1(row(D_{t-1}), r); afterwards `slot` describes row(D_t)
+  __device__ double resolve(const ExpArgs& a, const uint32_t (&key)[NW], uint32_t r) {
+    double lpv = a.lp_unseen;
+    int32_t ns = -2;
+    if (slot >= 0) {
+      lpv = plp; ns = pnx;
+    } else if (cand) {
+      if (same_key(pkey, key)) {
+        lpv = plp; ns = pnx;
+      } else if (pkey[0] != kEmptyKey) {
+        // home slot holds another row: linear probing up to an empty slot
+        uint32_t sl = hs;
+        bool found = false;
+        for (int pr = 1; pr <= a.max_probe; ++pr) {
+          sl = (sl + 1u) & a.hmask;
+          uint32_t k[NW];
+#pragma unroll
+          for (int w = 0; w < NW; ++w) k[w] = ld_off<uint32_t>(a.hkey, (sl * NW + w) * 4u);
+          if (k[0] == kEmptyKey) break;
+          if (same_key(k, key)) { found = true; break; }
+        }
+        if (found) {
+          lpv = ld_off<double>(a.hrow, sl * RSB + 8u * r);
+          ns = ld_off<int32_t>(a.hrow, sl * RSB + 4u * (2u * R + r));
+        }
+      }
+    }
+    slot = ns;
+    return lpv;
+  }
+  // D_t's key is known: issue the next step's loads
+  __device__ void prefetch(const ExpArgs& a, const uint32_t (&key)[NW], uint32_t rn) {
+    if (slot >= 0) {
+      prefetch_row(a, slot, rn);
+    } else if (slot == -2) {
+      uint32_t h1, h2, wi;
+      key_hash(key, NW, h1, h2);
+      hs = h1 & a.hmask;
+      filter_probe(h1, h2, a.fmask, wi, flo, fhi);
+      // one 8-byte load into both halves (two dword loads into two fields would
+      // be sunk with prefetch_row's stores behind a pointer phi: scratch)
+      const uint64_t f = ld_off<uint64_t>(a.filt, wi * 8u);
+      fw = make_uint2((uint32_t)f, (uint32_t)(f >> 32));
+    }
+  }
+};
+
+// D_t of one sequence as 2^m bytes in canonical state order, from nibble keys
+// in the device layout (key_nibble)
+template <int m>
+__device__ __forceinline__ void k1b_trace(uint8_t* tr, int64_t t, int64_t nseq, int64_t q,
+                                          const uint32_t (&key)[(1 << m) / 8]) {
+  constexpr int M = 1 << m;
+  uint8_t* o = tr + ((size_t)t * nseq + q) * M;
+#pragma unroll
+  for (int s = 0; s < M; ++s) o[s] = (uint8_t)((key[s >> 3] >> (4 * cvd::key_nibble(M, s))) & 15u);
+}
+
+// ──────── k = 1, n = 2 single-vector kernel (standard butterfly; m = 6 headline) ────────
+//
+// For codes whose tap-0 and tap-m columns are both 11 (every good rate-1/2 code,
+// (133,171) and (7,5) included), the two ACS candidates of new states (2j, 2j+1)
+// come from D(j) with metrics (e, 2-e) and from D(j + 2^(m-1)) with (2-e, e),
+// e = popcount(out(j, 0) ^ y).  The lane's own received word y picks e per
+// butterfly with ONE v_perm_b32 from a 4-byte constant, and one packed-16
+// add/add/min produces the pair (D(2j), D(2j+1)) -- the next step's operand, in
+// place.  Only D_t(y) itself is computed: 2^(m-1) butterflies of 4 packed VALU
+// ops, against 2 x 2^m ACS for the orbit kernel.
+//
+// T_ref count without the other words (exact, no fallback).  y ^ 3 flips every
+// e to 2 - e, so D_t(y ^ 3) is the pair swap of D_t(y).  For y' = y ^ 1 or
+// y ^ 2 the butterfly classes swap (e in {0, 2} <-> e' = 1), and in each
+// butterfly the word with e in {0, 2} must give A(2j) == A(2j+1), which holds
+// iff D_{t-1}(j) == D_{t-1}(j + 2^(m-1)).  So D_t(y') == D_t(y) (up to the
+// normalisation) needs equal halves; with equal halves d_j, A(2j) = A(2j+1) =
+// d_j + [e_j == 1] under y and d_j + [e_j != 1] under y', equal up to a constant
+// iff [e_j == 1] is constant over j, i.e. every out(j, 0) is in one class
+// (a property of the code only: bfly_uni).  Hence
+// c = 1 + [D_t(y) == pair swap] + 2 [halves equal and bfly_uni].
+//
+// Dp carries the metric pairs plus a per-lane offset O (the sum of the step
+// minima since the last renormalisation, every kRenorm steps); nibble keys are
+// formed with two shift-adds per 4 butterflies and the offset removed by one
+// subtraction per word (exact modulo 2^32).  The step minimum is 0 or 1
+// (n = 2; D_{t-1} has a 0 state and one of its branches has metric <= 1), so it
+// is read off a zero-nibble test.
+constexpr int kK1bWavesPerSimd = 5;
+constexpr int kRenorm = 128;   // O <= 128: raw pair values stay < 256 (byte packing)
+
+// The common step: D_t(y) for the lane's own word, in place in Dp (pair i is
+// dead once butterflies 2i, 2i + 1 and 2i - H, 2i + 1 - H have read it), and
+// the nibble keys of the raw metrics minus the running offset.
+template <int m, bool kSpec, uint64_t XM>
+__device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1 << m) / 8, 4>& cur, uint32_t rr,
+                                        uint32_t (&Dp)[(1 << m) / 2], uint32_t (&kw)[(1 << m) / 8],
+                                        uint32_t sel, uint32_t O8, uint32_t& zn) {
+  constexpr int M = 1 << m, H = M / 2;
+  uint32_t E[H];
+  // specialised (kSpec, out(j, 0) = bits 2j..2j+1 of XM): the lane's pairs
+  // (e, 2 - e) for out(j, 0) = 0 and 1; out 3 and 2 are their swaps (op_sel),
+  // so no table and no v_perm per butterfly
+  uint32_t W0 = 0u, W1 = 0u;
+  if constexpr (kSpec) {
+    const uint32_t e0 = __builtin_popcount(rr), e1 = __builtin_popcount(rr ^ 1u);
+    W0 = e0 | ((2u - e0) << 16);
+    W1 = e1 | ((2u - e1) << 16);
+  }
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    if (j == H / 2) {                   // filter positive: key + row loads under the second half
+      cur.fence(zn);                    // zn depends on every butterfly so far
+      cur.mid(a, rr);
+    }
+    const us2 pa = as_us2(Dp[j >> 1]), pb = as_us2(Dp[(j >> 1) + H / 2]);
+    const us2 da = (j & 1) ? __builtin_shufflevector(pa, pa, 1, 1) : __builtin_shufflevector(pa, pa, 0, 0);
+    const us2 db = (j & 1) ? __builtin_shufflevector(pb, pb, 1, 1) : __builtin_shufflevector(pb, pb, 0, 0);
+    us2 W;
+    if constexpr (kSpec) {
+      const int xj = (int)((XM >> (2 * j)) & 3u);
+      W = xj == 0 ? as_us2(W0) : xj == 1 ? as_us2(W1) : xj == 2 ? __builtin_shufflevector(as_us2(W1), as_us2(W1), 1, 0)
+                                                             : __builtin_shufflevector(as_us2(W0), as_us2(W0), 1, 0);
+    } else {
+      const uint32_t T = tb[j];
+      W = as_us2(__builtin_amdgcn_perm(T, T, sel));   // (e, 2 - e)
+    }
+    E[j] = as_u32(__builtin_elementwise_min(da + W, db + __builtin_shufflevector(W, W, 1, 0)));
+    if ((j & 3) == 3) {
+      // word w = states 8w..8w+7 in nibble order bitrev3 (device key layout):
+      // bytes (E0.lo, E1.lo, E0.hi, E1.hi) by one v_perm (metrics + O < 256)
+      const uint32_t x = __builtin_amdgcn_perm(E[j - 2], E[j - 3], 0x06020400u);
+      const uint32_t y = __builtin_amdgcn_perm(E[j], E[j - 1], 0x06020400u);
+      const uint32_t v = x + (y << 4) - O8;             // nibbles = raw metric - offset <= 14
+      zn |= (v - 0x11111111u) & ~v;
+      kw[j >> 2] = v;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < H; ++j) Dp[j] = E[j];
+}
+
+template <int m, bool kSpec, uint64_t XM>
+__device__ __forceinline__ void k1b_body(const ExpArgs& a) {
+  constexpr int M = 1 << m, H = M / 2, NW = M / 8, R = 4;
+  static_assert(m >= 3, "k1b kernel: 2^m >= 8 (whole key words)");
+  __shared__ double s_lt[R + 1];
+  if (threadIdx.x <= R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  __syncthreads();
+  // Sequence index without a VGPR live across the step loop: the wave's first
+  // index in SGPRs, the lane from mbcnt, recomputed after the loop; validity
+  // and hypothesis as wave ballots (SGPRs)
+  const int64_t qwave = (int64_t)blockIdx.x * kBlock + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const int64_t q = qwave + lane_id();
+  const bool valid = q < a.nseq;
+  const uint64_t vmask = __ballot(valid), hmask = __ballot(q < a.n_h1);
+  double lp = 0.0, lr = 0.0;
+  if (valid) {
+    uint32_t Dp[H];   // (D(2i), D(2i+1)) + O, packed 16-bit
+#pragma unroll
+    for (int i = 0; i < H; ++i) Dp[i] = 0u;
+    uint32_t key[NW];  // normalised D_{t-1}, device key layout
+#pragma unroll
+    for (int w = 0; w < NW; ++w) key[w] = 0u;
+    uint32_t O = 0u, O8 = 0u;   // O8 = O * 0x11111111
+    if (a.trace) k1b_trace<m>(a.trace, 0, a.nseq, q, key);
+    StreamReader<2> rd;
+    rd.init(a.r, a.nseq, q, a.N);
+    RowCursor<NW, R> cur;
+    cur.start(a, rd.peek());
+    for (int64_t t = 1; t <= a.N; ++t) {
+      const uint32_t rr = rd.peek();
+      const uint32_t rn = t < a.N ? rd.peek_next() : 0u;
+      // halves differences of D_{t-1}: nibble of state j (< 2^(m-1)) is nonzero
+      // iff D_{t-1}(j) != D_{t-1}(j + 2^(m-1))
+      constexpr int NH = NW >= 2 ? NW / 2 : 1;
+      uint32_t dh[NH];
+      if constexpr (NW >= 2) {
+#pragma unroll
+        for (int w = 0; w < NH; ++w) dh[w] = key[w] ^ key[w + NH];
+      } else {
+        dh[0] = (key[0] ^ (key[0] >> 4)) & 0x0F0F0F0Fu;   // states s, s + 4 = nibbles 2i, 2i + 1
+      }
+      uint32_t hx = 0u, se = 0u, so = 0u;
+#pragma unroll
+      for (int w = 0; w < NH; ++w) {
+        hx |= dh[w];
+        se |= dh[w] & a.bfly_even[w];
+        so |= dh[w] & ~a.bfly_even[w];
+      }
+      // D_t(y) == its pair swap iff D_{t-1}(j) == D_{t-1}(j + 2^(m-1)) for every
+      // butterfly with e_j in {0, 2}, i.e. out(j, 0) in the class of y
+      const uint32_t sym = (__builtin_popcount(rr) & 1u) ? so : se;
+      const uint32_t sel = rr | ((rr ^ 3u) << 16) | 0x0C000C00u;
+      cu32* tb = as_const(a.bmp);
+      asm volatile("" : "+s"(tb));   // per step: the table is re-read (scalar cache), not held in SGPRs
+      uint32_t kw[NW];
+      uint32_t zn = 0u;
+      k1b_acs<m, kSpec, XM>(a, tb, cur, rr, Dp, kw, sel, O8, zn);
+      // Eq. 5: step minimum 0 or 1
+      const uint32_t mu = (zn & 0x88888888u) == 0u;
+      const uint32_t mu8 = mu ? 0x11111111u : 0u;
+      O += mu;
+      O8 += mu8;
+      // P̂1 row of D_{t-1}
+      cur.fence(zn);                          // zn depends on the whole ACS
+      cur.template fence_keys<NW>(zn);
+      lp += cur.resolve(a, key, rr);          // Pd_plotter.py:115, T = P̂1
+#pragma unroll
+      for (int w = 0; w < NW; ++w) key[w] = kw[w] - mu8;
+      // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni
+      const uint32_t c = 1u + (sym == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
+      lr += s_lt[c];                          // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
+      if (a.trace) k1b_trace<m>(a.trace, t, a.nseq, q, key);
+      cur.prefetch(a, key, rn);
+      rd.advance();
+      if ((t & (kRenorm - 1)) == 0) {
+        const us2 o2 = as_us2(O * 0x10001u);
+#pragma unroll
+        for (int i = 0; i < H; ++i) Dp[i] = as_u32(as_us2(Dp[i]) - o2);
+        O = 0u;
+        O8 = 0u;
+      }
+    }
+    if (a.sums) {
+      const int64_t qe = qwave + lane_id();
+      a.sums[2 * qe] = lp;
+      a.sums[2 * qe + 1] = lr;
+    }
+  }
+  count_decisions_masked(vmask, hmask, lp, lr, a.counts);
+}
+
+}  // namespace cvd_dev

@@ -455,11 +455,13 @@ void build_bfly(cvd_model& Mo, const Tabs& T) {
   }
   Mo.bfly.assign((size_t)H, 0u);
   Mo.bfly_uni = 1u;
+  Mo.bfly_x = 0u;
   for (uint32_t& w : Mo.bfly_even) w = 0u;
   for (int j = 0; j < H; ++j) {
     const uint32_t x = T.out[j * T.K + 0];
     for (uint32_t y = 0; y < 4; ++y) Mo.bfly[(size_t)j] |= (uint32_t)__builtin_popcount(x ^ y) << (8 * y);
     // class of out(j, 0): {00, 11} or {01, 10}; out(0, 0) = 00
+    Mo.bfly_x |= (uint64_t)x << (2 * j);
     if (__builtin_popcount(x) & 1) Mo.bfly_uni = 0u;
     // nibble of state j in the halves-difference words (device key layout)
     else Mo.bfly_even[j / 8] |= 0xFu << (4 * key_nibble(T.M, j));

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "cvd_common.h"
+#include "cvd_keys.h"
 
 struct cvd_model {
   cvd::CodeDesc dec;          // decoder trellis (G1; Pd_plotter.py:188 "decoder is fixed to H1")
@@ -47,6 +48,8 @@ struct cvd_model {
   bool k1b_ok = false;
   uint32_t bfly_uni = 0;           // every out(j, 0), j < 2^(m-1), in {00, 11}
   uint32_t bfly_even[4] = {0, 0, 0, 0};   // nibble masks of the butterflies j with out(j, 0) in {00, 11}
+  uint64_t bfly_x = 0;             // out(j, 0) in bits 2j..2j+1 (the specialisation key)
+  void* rtc_fn = nullptr;          // hipFunction_t of the specialised kernel on `device`, if built
   std::vector<uint32_t> bfly;      // [2^m / 2]
 
   // device copies
@@ -66,54 +69,10 @@ namespace cvd {
 
 void set_error(const std::string& msg);
 inline int nib_words(int m) { return (1 << m) >= 8 ? (1 << m) / 8 : 1; }
-// row record: 2^n doubles + 2^n int32 successor slots, padded to a power of
-// two (64 B at n = 2: one record never straddles a cache line)
-constexpr int row_words_c(int R) { return 3 * R <= 4 ? 4 : 2 * row_words_c((R + 1) / 2); }
 CVD_HD int row_words(int n) { return row_words_c(1 << n); }
 
 // Nibble packing of a metric vector: state s in nibble s (word s / 8, bits 4*(s % 8)).
 void pack_nibbles(const uint8_t* D, int M, uint32_t* out);
-
-// Device key layout (hash keys, row cursor) for 2^m >= 8: inside each 32-bit
-// word, state 8w + s sits in nibble bitrev3(s) -- the order in which a lane's
-// packed (D(2j), D(2j+1)) pairs collapse into nibbles with two shift-adds.
-// key_swap converts either way (an involution: nibbles 1 <-> 4, 3 <-> 6).
-CVD_HD uint32_t key_swap(uint32_t w) {
-  const uint32_t t = (w ^ (w >> 12)) & 0x0000F0F0u;
-  return w ^ t ^ (t << 12);
-}
-CVD_HD int key_nibble(int M, int s) {   // nibble index of state s within its word
-  const int b = s & 7;
-  return M >= 8 ? (((b & 1) << 2) | (b & 2) | ((b >> 2) & 1)) : b;
-}
-
-// 32-bit hash pair of a nibble-packed key; must match the device version.
-// A rotate/xor-add fold (2 full-rate VALU ops per word) and two finalising
-// multiplies; h1 picks the slot, h2 is the fingerprint.
-CVD_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-CVD_HD void key_hash(const uint32_t* w, int nw, uint32_t& h1, uint32_t& h2) {
-  uint32_t h = 0x9E3779B9u ^ (uint32_t)nw;
-  for (int i = 0; i < nw; ++i) h = (h ^ w[i]) + rotl32(h, 25);
-  uint32_t a = h * 0x85EBCA6Bu;
-  h1 = a ^ (a >> 16);
-  uint32_t b = (h ^ (h >> 13)) * 0xC2B2AE35u;
-  h2 = b ^ (b >> 15);
-}
-
-// Blocked Bloom filter over the row keys (explicit path): one 64-bit word per
-// key, two bits in each 32-bit half.  A lookup of a state that is not a row
-// (most lookups at p >= 0.05 and for every H2 sequence) ends on this one
-// L2-resident load.  Word index from h2, bit positions from a third mix.
-CVD_HD void filter_probe(uint32_t h1, uint32_t h2, uint32_t fmask, uint32_t& wi, uint32_t& lo,
-                         uint32_t& hi) {
-  wi = h2 & fmask;
-  const uint32_t h3 = (h1 ^ rotl32(h2, 16)) * 0x9E3779B1u;
-  lo = (1u << (h3 >> 27)) | (1u << ((h3 >> 22) & 31u));
-  hi = (1u << ((h3 >> 17) & 31u)) | (1u << ((h3 >> 12) & 31u));
-}
-// empty hash slot: key word 0 (a nibble-packed metric vector never has 15 in
-// every nibble, metrics stay <= (ceil(m/k)+1) n - 1 <= 14)
-constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;
 
 // kernel launchers (cvd_kernels.hip)
 int launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, uint64_t thr,
@@ -125,10 +84,12 @@ int launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, i
                            int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
                            void* stream, int variant);
 // launch_detect_explicit variants
-constexpr int kExplicitBest = 0, kExplicitOrbit = 1, kExplicitGeneric = 2;
+constexpr int kExplicitBest = 0, kExplicitOrbit = 1, kExplicitGeneric = 2, kExplicitButterfly = 3;
 int upload_model(cvd_model& M, int device);
 // CVD_KERNEL_* that launch_detect_explicit(kExplicitBest) picks for this model
 int explicit_kernel_of(const cvd_model& M);
+// hipRTC-compiled code-specialised butterfly kernel (cvd_rtc.cpp); 0 = ok
+int rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);
 

@@ -1,0 +1,68 @@
+// Row-key definitions shared by the host table build (cvd_host.cpp), the
+// compiled kernels (cvd_kernels.hip) and the kernels hipRTC specialises at run
+// time (cvd_device.h): self-contained, no standard-library includes.
+#pragma once
+
+#ifndef CVD_HD
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+#define CVD_HD __host__ __device__ __forceinline__
+#else
+#define CVD_HD inline
+#endif
+#endif
+
+namespace cvd {
+
+// row record: 2^n doubles + 2^n int32 successor slots, padded to a power of
+// two (64 B at n = 2: one record never straddles a cache line)
+constexpr int row_words_c(int R) { return 3 * R <= 4 ? 4 : 2 * row_words_c((R + 1) / 2); }
+
+// Device key layout (hash keys, row cursor) for 2^m >= 8: inside each 32-bit
+// word, state 8w + s sits in nibble bitrev3(s) -- the order in which a lane's
+// packed (D(2j), D(2j+1)) pairs collapse into nibbles with one v_perm and one
+// shift-add.  key_swap converts either way (an involution: nibbles 1 <-> 4, 3 <-> 6).
+CVD_HD unsigned key_swap(unsigned w) {
+  const unsigned t = (w ^ (w >> 12)) & 0x0000F0F0u;
+  return w ^ t ^ (t << 12);
+}
+CVD_HD int key_nibble(int M, int s) {   // nibble index of state s within its word
+  const int b = s & 7;
+  return M >= 8 ? (((b & 1) << 2) | (b & 2) | ((b >> 2) & 1)) : b;
+}
+
+CVD_HD unsigned rotl32(unsigned x, int r) { return (x << r) | (x >> (32 - r)); }
+CVD_HD unsigned long long mul_wide(unsigned a, unsigned b) { return (unsigned long long)a * b; }
+
+// 32-bit hash pair of a nibble-packed key (host and device must agree).  A
+// multiply-accumulate fold, one v_mad_u64_u32 per key word with a distinct odd
+// multiplier, then two 32x32->64 finalising products folded hi ^ lo; h1 picks
+// the home slot, h2 the filter word.  Quality only affects speed (probe
+// lengths, filter false positives), never results.
+CVD_HD void key_hash(const unsigned* w, int nw, unsigned& h1, unsigned& h2) {
+  unsigned long long acc = 0x9E3779B97F4A7C15ull ^ (unsigned)nw;
+  for (int i = 0; i < nw; ++i) acc += mul_wide(w[i], 0x85EBCA77u + 0x6A09E668u * (unsigned)i);
+  const unsigned x = (unsigned)acc ^ (unsigned)(acc >> 32);
+  const unsigned long long p = mul_wide(x, 0x85EBCA6Bu);
+  h1 = (unsigned)p ^ (unsigned)(p >> 32);
+  const unsigned long long q = mul_wide(x ^ (x >> 16), 0xC2B2AE35u);
+  h2 = (unsigned)q ^ (unsigned)(q >> 32);
+}
+
+// Blocked Bloom filter over the row keys (explicit path): one 64-bit word per
+// key, two bits in each 32-bit half.  A lookup of a state that is not a row
+// (most lookups at p >= 0.05 and for every H2 sequence) ends on this one
+// L2-resident load.  Word index from h2, bit positions from a third mix (the
+// shift counts are the low 5 bits of shifted copies, as v_lshlrev reads them).
+CVD_HD void filter_probe(unsigned h1, unsigned h2, unsigned fmask, unsigned& wi, unsigned& lo,
+                         unsigned& hi) {
+  wi = h2 & fmask;
+  const unsigned h3 = (h1 ^ rotl32(h2, 16)) * 0x9E3779B1u;
+  lo = (1u << (h3 & 31u)) | (1u << ((h3 >> 5) & 31u));
+  hi = (1u << ((h3 >> 10) & 31u)) | (1u << ((h3 >> 15) & 31u));
+}
+
+// empty hash slot: key word 0 (a nibble-packed metric vector never has 15 in
+// every nibble, metrics stay <= (ceil(m/k)+1) n - 1 <= 14)
+constexpr unsigned kEmptyKey = 0xFFFFFFFFu;
+
+}  // namespace cvd

@@ -1,0 +1,182 @@
+// Code-specialised butterfly detector kernels, compiled at run time.
+//
+// The k = 1, n = 2 butterfly kernel (cvd_device.h) reads each butterfly's
+// branch-metric pair from a per-code table with one v_perm_b32.  With the
+// decoder code known at compile time the pair is one of four per-step
+// registers chosen statically, which removes 2^(m-1) v_perm and the table's
+// scalar loads per step.  The decoder is a run-time input (any G1), so the
+// specialised kernel is compiled here, once per (device, m, code) per
+// process, from the same device source the library is built from (embedded
+// by embed_src.py), and loaded as a module.
+//
+// Compiler: the ROCm toolchain's clang (device-only compile of one kernel,
+// about a second), so the code is produced by the same compiler as the
+// library.  hipRTC is the fallback: inside a PyTorch process it resolves to
+// the comgr bundled with torch (an older LLVM), whose code for this kernel
+// spills and runs ~25% slower than the table-driven kernel -- so it is only
+// used when no clang is found.  If both fail, the launcher keeps the compiled
+// table-driven kernel (same results, slower).
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+#include <fcntl.h>
+#include <spawn.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "cvd_internal.h"
+
+#include "cvd_rtc_src.inc"
+
+extern char** environ;
+
+namespace {
+
+std::mutex g_mu;
+std::map<std::tuple<int, int, uint64_t>, hipFunction_t> g_cache;
+
+std::string entry_source(int m, uint64_t xm) {
+  char entry[256];
+  std::snprintf(entry, sizeof(entry),
+                "\nextern \"C\" __global__ __launch_bounds__(cvd_dev::kBlock, cvd_dev::kK1bWavesPerSimd)\n"
+                "void cvd_k1b_spec(cvd_dev::ExpArgs a) { cvd_dev::k1b_body<%d, true, 0x%016llxull>(a); }\n",
+                m, (unsigned long long)xm);
+  return entry;
+}
+
+bool file_exists(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0;
+}
+
+std::string find_clang() {
+  if (const char* e = std::getenv("CVD_JIT_CLANG")) return e;
+  std::vector<std::string> cands;
+  if (const char* r = std::getenv("ROCM_PATH")) cands.push_back(std::string(r) + "/lib/llvm/bin/clang++");
+  cands.push_back("/opt/rocm/lib/llvm/bin/clang++");
+  cands.push_back("/opt/rocm/llvm/bin/clang++");
+  for (const auto& c : cands)
+    if (file_exists(c)) return c;
+  return "";
+}
+
+// device-only compile with the toolchain clang -> code object bytes
+bool compile_clang(const std::string& src, const std::string& arch, std::vector<char>& code, std::string& err) {
+  const std::string clang = find_clang();
+  if (clang.empty()) { err = "no clang++ found (set CVD_JIT_CLANG)"; return false; }
+  char dir_t[] = "/tmp/cvd_jit_XXXXXX";
+  const char* dir = ::mkdtemp(dir_t);
+  if (!dir) { err = "mkdtemp failed"; return false; }
+  const std::string d(dir), in = d + "/k1b_spec.hip", out = d + "/k1b_spec.co", log = d + "/log.txt";
+  {
+    std::ofstream f(in);
+    f << "#include <hip/hip_runtime.h>\n" << src;
+  }
+  const std::string arch_opt = "--offload-arch=" + arch;
+  std::vector<std::string> args = {clang, "-x", "hip", arch_opt, "--offload-device-only", "--no-gpu-bundle-output",
+                                   "-O3", "-std=c++17", "-ffp-contract=off", "-c", in, "-o", out};
+  std::vector<char*> argv;
+  for (auto& s : args) argv.push_back(&s[0]);
+  argv.push_back(nullptr);
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_addopen(&fa, 1, log.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  posix_spawn_file_actions_adddup2(&fa, 1, 2);
+  pid_t pid = 0;
+  int status = -1;
+  const int rc = ::posix_spawn(&pid, clang.c_str(), &fa, nullptr, argv.data(), environ);
+  posix_spawn_file_actions_destroy(&fa);
+  if (rc == 0) ::waitpid(pid, &status, 0);
+  bool ok = rc == 0 && WIFEXITED(status) && WEXITSTATUS(status) == 0;
+  if (ok) {
+    std::ifstream f(out, std::ios::binary);
+    code.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    ok = !code.empty();
+  }
+  if (!ok) {
+    std::ifstream f(log);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    err = "clang failed: " + ss.str().substr(0, 2000);
+  }
+  ::unlink(in.c_str()); ::unlink(out.c_str()); ::unlink(log.c_str()); ::rmdir(dir);
+  return ok;
+}
+
+bool compile_hiprtc(const std::string& src, const std::string& arch, std::vector<char>& code, std::string& err) {
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "cvd_k1b_spec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    err = "hiprtcCreateProgram failed";
+    return false;
+  }
+  const std::string arch_opt = "--offload-arch=" + arch;
+  const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    hiprtcDestroyProgram(&prog);
+    err = std::string("hipRTC compile failed: ") + hiprtcGetErrorString(rc) + "\n" + log.substr(0, 2000);
+    return false;
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  code.resize(n);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  return n > 0;
+}
+
+}  // namespace
+
+// hipFunction_t of cvd_k1b_spec<m, code> on `device`, compiling it on first use.
+int cvd::rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out) {
+  *fn_out = nullptr;
+  if (const char* e = std::getenv("CVD_NO_JIT"))
+    if (e[0] && e[0] != '0') { set_error("JIT: disabled by CVD_NO_JIT"); return -1; }
+  std::lock_guard<std::mutex> lock(g_mu);
+  const auto key = std::make_tuple(device, m, xm);
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) {
+    *fn_out = (void*)it->second;
+    return 0;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_error("JIT: device properties"); return -1; }
+  std::string arch = prop.gcnArchName;
+  const size_t colon = arch.find(':');
+  if (colon != std::string::npos) arch = arch.substr(0, colon);
+
+  const std::string src = std::string(kRtcSource) + entry_source(m, xm);
+  std::vector<char> code;
+  std::string err1, err2;
+  const char* via = std::getenv("CVD_JIT_VIA");   // "hiprtc" forces the fallback (tests)
+  const bool ok = (!(via && std::string(via) == "hiprtc") && compile_clang(src, arch, code, err1)) ||
+                  compile_hiprtc(src, arch, code, err2);
+  if (!ok) { set_error("JIT: " + err1 + " | " + err2); return -1; }
+
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(device);
+  hipModule_t mod;
+  hipFunction_t fn;
+  const bool loaded = hipModuleLoadData(&mod, code.data()) == hipSuccess &&
+                      hipModuleGetFunction(&fn, mod, "cvd_k1b_spec") == hipSuccess;
+  (void)hipSetDevice(cur);
+  if (!loaded) { set_error("JIT: module load failed"); return -1; }
+  g_cache[key] = fn;   // modules live for the process (one per device and code)
+  *fn_out = (void*)fn;
+  return 0;
+}

@@ -75,6 +75,7 @@ typedef struct cvd_model_info {
 #define CVD_KERNEL_GENERIC 1    /* detect_explicit_kernel<m,k,n>: ACS for every received word */
 #define CVD_KERNEL_ORBIT 2      /* detect_k1_kernel<m,n>: k = 1, ACS for the 2^n/2 orbit representatives */
 #define CVD_KERNEL_BUTTERFLY 3  /* detect_k1b_kernel<m>: k = 1, n = 2 standard butterflies, one ACS vector */
+#define CVD_KERNEL_BUTTERFLY_RTC 4  /* the same, specialised to the decoder code at model upload (JIT, cvd_rtc.cpp) */
 
 typedef struct cvd_model cvd_model;
 
@@ -128,6 +129,7 @@ int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int
 #define CVD_PATH_EXPLICIT 2  /* explicit 2^m metric vector + hashed P̂1 rows (fastest k=1 kernel that applies) */
 #define CVD_PATH_EXPLICIT_GENERIC 3  /* explicit path, ACS for every received word (no orbit reduction) */
 #define CVD_PATH_EXPLICIT_ORBIT 4    /* explicit path, k=1 two-representative orbit kernel */
+#define CVD_PATH_EXPLICIT_BUTTERFLY 5  /* explicit path, k=1 n=2 butterfly kernel, table-driven (not code-specialised) */
 
 /* Detector over sequences 0..nseq-1 (pitch = nseq): per sequence the sequential
  * fp64 sums log P̂1(D_0^N) and log T_ref(D_0^N) (Pd_plotter.py:106-116); sequences

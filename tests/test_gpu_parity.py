@@ -272,10 +272,13 @@ def test_k1_kernels_intermediate_memory(pkg, dev, m, N, p):
 def _three_explicit_paths_agree(pkg, k, n, m, t1, t2, N, p, learn_len=None):
     det = pkg.Detector(k, n, m, t1, device=0)
     model = det.model(p, 20000 if m == 6 else learn_len, 200, 1.0, 77)
-    runs = {path: det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=path, return_sums=True)
-            for path in (pkg.PATH_EXPLICIT, pkg.PATH_EXPLICIT_ORBIT, pkg.PATH_EXPLICIT_GENERIC)}
+    paths = (pkg.PATH_EXPLICIT, pkg.PATH_EXPLICIT_BUTTERFLY, pkg.PATH_EXPLICIT_ORBIT, pkg.PATH_EXPLICIT_GENERIC)
+    runs = {path: det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=path, return_sums=True) for path in paths}
+    if k == 1 and n == 2 and m >= 3:
+        # standard butterflies: the default explicit kernel is the hipRTC-specialised one
+        assert model.info()["explicit_kernel"] == 4, pkg.lib().cvd_last_error()
     a = runs[pkg.PATH_EXPLICIT]
-    for path in (pkg.PATH_EXPLICIT_ORBIT, pkg.PATH_EXPLICIT_GENERIC):
+    for path in paths[1:]:
         assert np.array_equal(a["sums"], runs[path]["sums"]), path
         assert a["counts"].cpu().tolist() == runs[path]["counts"].cpu().tolist(), path
     if m < 6 and model.info()["kind"] == 0:
