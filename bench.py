@@ -137,12 +137,13 @@ def main():
     # received streams read once, 2 * ceil(N * n / 8) bytes per trial
     alg_bytes = B * 2 * ((N * n + 7) // 8)
     achieved = alg_bytes / (det_ms * 1e-3) / 1e9
-    traffic, traffic_src = None, None
+    traffic, traffic_src, valu = None, None, None
     if a.pmc_traffic and os.path.exists(a.pmc_traffic):
         with open(a.pmc_traffic) as f:
             pmc = json.load(f)
         if (pmc.get("config"), pmc.get("batch"), pmc.get("N")) == (a.config, B, N):
             traffic = pmc.get("detector_fetch_bytes_per_launch")
+            valu = {k: pmc.get(k) for k in ("VALU_insts_per_wave_step", "valu_issue_frac_est", "kernel")}
             traffic_src = os.path.relpath(a.pmc_traffic, ROOT) + " (rocprofv3 FETCH_SIZE x1024 x2, gfx950 correction)"
     c = counts.cpu().numpy()
     per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, (a.steps // len(p_grid) + (i < a.steps % len(p_grid))) * B * world),
@@ -176,6 +177,8 @@ def main():
                        "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
                        "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
                        "detector_ms_steps": det_each,
+                       # the binding resource is VALU issue, not HBM: from the PMC summary
+                       "valu_bound": valu,
                        "per_p": per_p},
     }
     if a.cpu_baseline and world == 1:

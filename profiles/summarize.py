@@ -1,0 +1,88 @@
+"""Turn a profiles/collect.sh output directory (gpurun_out/...) into the
+committed evidence: profiles/<name>/ (rocprofv3 kernel stats, trace and PMC
+CSVs trimmed to the detector and generator) and profiles/detector_pmc.json,
+which bench.py reads for roofline.traffic.
+
+  python profiles/summarize.py gpurun_out/prof r01c
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def is_det(name):
+    return "detect" in name or "k1b" in name
+
+
+def main(src, name):
+    dst = os.path.join(ROOT, "profiles", name)
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))[0]
+    shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+    trace = glob.glob(os.path.join(src, "trace", "*kernel_trace.csv"))[0]
+    rows = [r for r in csv.DictReader(open(trace)) if is_det(r["Kernel_Name"]) or "gen_kernel" in r["Kernel_Name"]]
+    with open(os.path.join(dst, "kernel_trace.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+        w.writeheader()
+        w.writerows(rows)
+    bench = json.load(open(os.path.join(src, "bench_trace.json")))
+    json.dump(bench, open(os.path.join(dst, "bench_under_rocprof.json"), "w"), indent=1)
+    agg, cnt = {}, {}
+    for i, f in enumerate(sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")))):
+        keep = [r for r in csv.DictReader(open(f)) if is_det(r["Kernel_Name"]) or "gen_kernel" in r["Kernel_Name"]]
+        tag = os.path.basename(os.path.dirname(f))
+        with open(os.path.join(dst, f"{tag}.csv"), "w", newline="") as g:
+            w = csv.DictWriter(g, fieldnames=list(keep[0].keys()))
+            w.writeheader()
+            w.writerows(keep)
+        for r in keep:
+            if is_det(r["Kernel_Name"]):
+                k = r["Counter_Name"]
+                agg[k] = agg.get(k, 0.0) + float(r["Counter_Value"])
+                cnt[k] = cnt.get(k, 0) + 1
+    per = {k: agg[k] / cnt[k] for k in agg}
+    cfg = bench["config"]
+    B, N = cfg["trials_per_step_per_gpu"], cfg["N"]
+    waves = per.get("SQ_WAVES", 2 * B / 64)
+    kernel_cycles = per.get("GRBM_GUI_ACTIVE", 0.0) / 8   # GRBM_GUI_ACTIVE sums the 8 XCDs
+    out = {
+        "kernel": bench["roofline"]["kernel"],
+        "workload": f"bench.py --steps 2 --warmup 0 (p = 0.01, 0.02), {B} trials x 2 sequences, N = {N}",
+        "source": "rocprofv3 --pmc, one counter group per pass (profiles/collect.sh), averaged per detector launch",
+        "FETCH_SIZE_kB_per_launch": per.get("FETCH_SIZE"),
+        "WRITE_SIZE_kB_per_launch": per.get("WRITE_SIZE"),
+        "detector_fetch_bytes_per_launch_raw": per.get("FETCH_SIZE", 0.0) * 1024,
+        "detector_fetch_bytes_per_launch": per.get("FETCH_SIZE", 0.0) * 1024 * 2,
+        "correction": "x2 per MI355X_MICROARCH.md HBM section (FETCH_SIZE = half of a 16-B/lane streaming read); "
+                      "the row-table traffic is 8-64 B random accesses, which that guide leaves uncalibrated",
+        "algorithmic_bytes_per_launch": 2 * B * ((N * 2 + 7) // 8),
+        "SQ_INSTS_VALU_per_launch": per.get("SQ_INSTS_VALU"),
+        "VALU_insts_per_wave_step": per.get("SQ_INSTS_VALU", 0.0) / (waves * N),
+        "SALU_insts_per_wave_step": per.get("SQ_INSTS_SALU", 0.0) / (waves * N),
+        "VMEM_RD_insts_per_wave_step": per.get("SQ_INSTS_VMEM_RD", 0.0) / (waves * N),
+        "SQ_WAVES": waves,
+        "GRBM_GUI_ACTIVE": per.get("GRBM_GUI_ACTIVE"),
+        "kernel_cycles": kernel_cycles,
+        # VALU issue capacity: 1024 SIMDs, one wave64 instruction per 2 cycles (plain VOP2
+        # add/sub/logic/16-bit) or 4 cycles (VOP3/VOP3P/shifts: the packed ACS ops),
+        # measured on MI355X (.scratch microbenchmarks); the hot loop averages
+        # ~3.5 issue cycles per VALU instruction (static mix of the JIT kernel)
+        "valu_issue_frac_est": per.get("SQ_INSTS_VALU", 0.0) * 3.5 / (1024 * max(1.0, kernel_cycles)),
+        "wait_inst_any_frac_of_wave_cycles": per.get("SQ_WAIT_INST_ANY", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
+        "active_valu_frac_of_wave_cycles": per.get("SQ_ACTIVE_INST_VALU", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
+        "counters_per_launch": per,
+        "config": "m6",
+        "batch": B,
+        "N": N,
+    }
+    json.dump(out, open(os.path.join(ROOT, "profiles", "detector_pmc.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "counters_per_launch"}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
