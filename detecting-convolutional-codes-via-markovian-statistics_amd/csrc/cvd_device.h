@@ -59,6 +59,14 @@ __device__ __forceinline__ uint32_t next_word(const uint32_t* r, int64_t pitch, 
   return e == 0 ? cache.x : e == 1 ? cache.y : e == 2 ? cache.z : cache.w;
 }
 
+// 2-bit field of x at bit s, extracted where it is used: a volatile asm is not
+// hoisted, so the four steps of a group do not hold all their words live.
+__device__ __forceinline__ uint32_t bits2(uint32_t x, uint32_t s) {
+  uint32_t d;
+  asm volatile("v_bfe_u32 %0, %1, %2, 2" : "=v"(d) : "v"(x), "v"(s));
+  return d;
+}
+
 // Lane index in the wave (v_mbcnt; cheap to recompute instead of keeping live:
 // the laundered mask keeps LLVM from merging two calls and holding the first
 // result across the step loop).
@@ -297,7 +305,7 @@ __device__ __forceinline__ void k1b_trace(uint8_t* tr, int64_t t, int64_t nseq, 
 // subtraction per word (exact modulo 2^32).  The step minimum is 0 or 1
 // (n = 2; D_{t-1} has a 0 state and one of its branches has metric <= 1), so it
 // is read off a zero-nibble test.
-constexpr int kK1bWavesPerSimd = 5;
+constexpr int kK1bWavesPerSimd = 4;
 constexpr int kRenorm = 128;   // O <= 128: raw pair values stay < 256 (byte packing)
 
 // The common step: D_t(y) for the lane's own word, in place in Dp (pair i is
@@ -374,30 +382,41 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
 #pragma unroll
     for (int w = 0; w < NW; ++w) key[w] = 0u;
     uint32_t O = 0u, O8 = 0u;   // O8 = O * 0x11111111
-    if (a.trace) k1b_trace<m>(a.trace, 0, a.nseq, q, key);
-    StreamReader<2> rd;
-    rd.init(a.r, a.nseq, q, a.N);
+    if (a.trace) k1b_trace<m>(a.trace, 0, a.nseq, qwave + lane_id(), key);
+    // Received words: word w of this sequence at rbase + (w/4)*cstride + w%4
+    // (16-byte chunks, include/cvd.h).  Only the current word and the next are
+    // held; the next is loaded when the current one starts, 12 steps before its
+    // first use (the last group of the current word reads its first step).
+    const int64_t N = a.N, nwords = (N + 15) / 16;
+    const uint32_t* rbase = a.r + (size_t)(qwave + lane_id()) * 4;
+    const size_t cstride = (size_t)a.nseq * 4;   // dwords between chunks of one sequence
+    auto load_word = [&](int64_t wi) -> uint32_t {
+      return wi < nwords ? rbase[(size_t)(wi >> 2) * cstride + (size_t)(wi & 3)] : 0u;
+    };
+    uint32_t cw = load_word(0);     // current word
+    uint32_t nw = load_word(1);     // next word
+    int64_t w = 0;                  // index of the current word
     RowCursor<NW, R> cur;
-    cur.start(a, rd.peek());
-    for (int64_t t = 1; t <= a.N; ++t) {
-      const uint32_t rr = rd.peek();
-      const uint32_t rn = t < a.N ? rd.peek_next() : 0u;
+    cur.start(a, cw & 3u);
+
+    // one step t (1-based) with received word rr and the next step's word rn
+    auto step = [&](uint32_t rr, uint32_t rn, int64_t t) {
       // halves differences of D_{t-1}: nibble of state j (< 2^(m-1)) is nonzero
       // iff D_{t-1}(j) != D_{t-1}(j + 2^(m-1))
       constexpr int NH = NW >= 2 ? NW / 2 : 1;
       uint32_t dh[NH];
       if constexpr (NW >= 2) {
 #pragma unroll
-        for (int w = 0; w < NH; ++w) dh[w] = key[w] ^ key[w + NH];
+        for (int v = 0; v < NH; ++v) dh[v] = key[v] ^ key[v + NH];
       } else {
         dh[0] = (key[0] ^ (key[0] >> 4)) & 0x0F0F0F0Fu;   // states s, s + 4 = nibbles 2i, 2i + 1
       }
       uint32_t hx = 0u, se = 0u, so = 0u;
 #pragma unroll
-      for (int w = 0; w < NH; ++w) {
-        hx |= dh[w];
-        se |= dh[w] & a.bfly_even[w];
-        so |= dh[w] & ~a.bfly_even[w];
+      for (int v = 0; v < NH; ++v) {
+        hx |= dh[v];
+        se |= dh[v] & a.bfly_even[v];
+        so |= dh[v] & ~a.bfly_even[v];
       }
       // D_t(y) == its pair swap iff D_{t-1}(j) == D_{t-1}(j + 2^(m-1)) for every
       // butterfly with e_j in {0, 2}, i.e. out(j, 0) in the class of y
@@ -418,20 +437,41 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       cur.template fence_keys<NW>(zn);
       lp += cur.resolve(a, key, rr);          // Pd_plotter.py:115, T = P̂1
 #pragma unroll
-      for (int w = 0; w < NW; ++w) key[w] = kw[w] - mu8;
+      for (int v = 0; v < NW; ++v) key[v] = kw[v] - mu8;
       // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni
       const uint32_t c = 1u + (sym == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
       lr += s_lt[c];                          // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
-      if (a.trace) k1b_trace<m>(a.trace, t, a.nseq, q, key);
+      if (a.trace) k1b_trace<m>(a.trace, t, a.nseq, qwave + lane_id(), key);
       cur.prefetch(a, key, rn);
-      rd.advance();
-      if ((t & (kRenorm - 1)) == 0) {
+    };
+
+    // groups of 4 steps (a quarter word): the 10 bits they read (4 words and
+    // the next step's) come from one window; only the last group of a word
+    // needs the next word
+    int64_t t = 0;
+    int g = 0;
+    for (; t + 4 <= N; t += 4) {
+      const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(nw, cw, 24);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) step(bits2(win, 2 * i), bits2(win, 2 * i + 2), t + i + 1);
+      if (++g == 4) {
+        g = 0;
+        cw = nw;
+        ++w;
+        nw = load_word(w + 1);
+      }
+      if (((t + 4) & (kRenorm - 1)) == 0) {
         const us2 o2 = as_us2(O * 0x10001u);
 #pragma unroll
         for (int i = 0; i < H; ++i) Dp[i] = as_u32(as_us2(Dp[i]) - o2);
         O = 0u;
         O8 = 0u;
       }
+    }
+    // last 1-3 steps (inside the current group, so no renormalisation is due)
+    if (t < N) {
+      const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(nw, cw, 24);
+      for (int i = 0; t < N; ++i, ++t) step(bits2(win, 2 * i), bits2(win, 2 * i + 2), t + 1);
     }
     if (a.sums) {
       const int64_t qe = qwave + lane_id();
