@@ -24,7 +24,8 @@ namespace cvd_dev {
 using cvd::kEmptyKey;
 using cvd::row_words_c;
 using cvd::key_hash;
-using cvd::filter_probe;
+using cvd::filter_mix;
+using cvd::filter_bits;
 
 constexpr int kBlock = 256;
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -103,7 +104,7 @@ __device__ __forceinline__ void count_decisions(bool valid, bool is_h1, double l
 // ────────────────────────── explicit metric path ────────────────────────────
 
 struct ExpArgs {
-  const uint32_t* filt;     // [fmask + 1][2] Bloom filter words over the row keys (filter_probe)
+  const uint32_t* filt;     // [fmask + 1] Bloom filter words over the row keys (filter_bits)
   const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors, word 0 = kEmptyKey if empty
   const uint32_t* hrow;     // [hcap][row_words(n)]: log P̂1[r] (f64), successor slot[r] (i32, -1 = not a row)
   const double* ltref;      // [R + 1]
@@ -162,7 +163,7 @@ struct StreamReader {
 // lookup), the key and row entries of the home slot only on a positive answer
 // (mid-step), and the exact key compare, with linear probing past an occupied
 // home slot, happens when the step resolves.  slot: >= 0 known row, -1 known
-// unvisited row, -2 pending hash probe (hs, filter word fw, bits flo/fhi).
+// unvisited row, -2 pending hash probe (home slot hs, filter word fw, bit mix h3).
 // 32-bit byte offsets from a uniform base (global_load with an SGPR base: no
 // 64-bit address arithmetic per lane)
 template <typename T>
@@ -174,8 +175,7 @@ template <int NW, int R>
 struct RowCursor {
   static constexpr uint32_t RSB = 4u * row_words_c(R);   // record bytes
   int32_t slot, pnx;
-  uint32_t hs, flo, fhi;
-  uint2 fw;
+  uint32_t hs, h3, fw;
   bool cand;
   double plp;
   uint32_t pkey[NW];
@@ -185,7 +185,7 @@ struct RowCursor {
     pnx = ld_off<int32_t>(a.hrow, off + 4u * (2u * R + rn));
   }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
-    slot = a.slot0; hs = 0u; flo = fhi = 0u; fw = make_uint2(0u, 0u); cand = false;
+    slot = a.slot0; hs = 0u; h3 = 0u; fw = 0u; cand = false;
     prefetch_row(a, slot, r0);
   }
   // Ordering fences: nothing in mid() / resolve() depends on the ACS, so
@@ -195,7 +195,7 @@ struct RowCursor {
   // that consumes an ACS result (the running zero-nibble test, which depends on
   // every butterfly computed so far), so the waits land after that much work.
   __device__ void fence(uint32_t dep) {
-    asm volatile("" : "+v"(fw.x), "+v"(fw.y), "+v"(slot), "+v"(pnx), "+v"(plp) : "v"(dep));
+    asm volatile("" : "+v"(fw), "+v"(slot), "+v"(pnx), "+v"(plp) : "v"(dep));
   }
   template <int N_>
   __device__ void fence_keys(uint32_t dep) {
@@ -203,7 +203,8 @@ struct RowCursor {
     for (int w = 0; w < N_; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
   }
   __device__ void mid(const ExpArgs& a, uint32_t r) {
-    cand = slot == -2 && (fw.x & flo) == flo && (fw.y & fhi) == fhi;
+    const uint32_t fb = filter_bits(h3);
+    cand = slot == -2 && (fw & fb) == fb;
     if (cand) {
 #pragma unroll
       for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs * NW + w) * 4u);
@@ -254,14 +255,11 @@ struct RowCursor {
     if (slot >= 0) {
       prefetch_row(a, slot, rn);
     } else if (slot == -2) {
-      uint32_t h1, h2, wi;
+      uint32_t h1, h2;
       key_hash(key, NW, h1, h2);
       hs = h1 & a.hmask;
-      filter_probe(h1, h2, a.fmask, wi, flo, fhi);
-      // one 8-byte load into both halves (two dword loads into two fields would
-      // be sunk with prefetch_row's stores behind a pointer phi: scratch)
-      const uint64_t f = ld_off<uint64_t>(a.filt, wi * 8u);
-      fw = make_uint2((uint32_t)f, (uint32_t)(f >> 32));
+      h3 = filter_mix(h1, h2);
+      fw = ld_off<uint32_t>(a.filt, (h2 & a.fmask) * 4u);
     }
   }
 };
@@ -388,10 +386,10 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     // held; the next is loaded when the current one starts, 12 steps before its
     // first use (the last group of the current word reads its first step).
     const int64_t N = a.N, nwords = (N + 15) / 16;
-    const uint32_t* rbase = a.r + (size_t)(qwave + lane_id()) * 4;
     const size_t cstride = (size_t)a.nseq * 4;   // dwords between chunks of one sequence
-    auto load_word = [&](int64_t wi) -> uint32_t {
-      return wi < nwords ? rbase[(size_t)(wi >> 2) * cstride + (size_t)(wi & 3)] : 0u;
+    auto load_word = [&](int64_t wi) -> uint32_t {   // lane address recomputed: no live VGPR pair
+      const uint32_t* rb = a.r + (size_t)(wi >> 2) * cstride + (size_t)(wi & 3) + (size_t)qwave * 4;
+      return wi < nwords ? rb[lane_id() * 4u] : 0u;
     };
     uint32_t cw = load_word(0);     // current word
     uint32_t nw = load_word(1);     // next word
@@ -401,6 +399,21 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
 
     // one step t (1-based) with received word rr and the next step's word rn
     auto step = [&](uint32_t rr, uint32_t rn, int64_t t) {
+      const uint32_t sel = rr | ((rr ^ 3u) << 16) | 0x0C000C00u;
+      cu32* tb = as_const(a.bmp);
+      asm volatile("" : "+s"(tb));   // per step: the table is re-read (scalar cache), not held in SGPRs
+      uint32_t kw[NW];
+      uint32_t zn = 0u;
+      k1b_acs<m, kSpec, XM>(a, tb, cur, rr, Dp, kw, sel, O8, zn);
+      // Eq. 5: step minimum 0 or 1
+      const uint32_t mu = (zn & 0x88888888u) == 0u;
+      const uint32_t mu8 = mu ? 0x11111111u : 0u;
+      O += mu;
+      O8 += mu8;
+      // P̂1 row of D_{t-1}
+      cur.fence(zn);                          // zn depends on the whole ACS
+      cur.template fence_keys<NW>(zn);
+      lp += cur.resolve(a, key, rr);          // Pd_plotter.py:115, T = P̂1
       // halves differences of D_{t-1}: nibble of state j (< 2^(m-1)) is nonzero
       // iff D_{t-1}(j) != D_{t-1}(j + 2^(m-1))
       constexpr int NH = NW >= 2 ? NW / 2 : 1;
@@ -421,21 +434,6 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       // D_t(y) == its pair swap iff D_{t-1}(j) == D_{t-1}(j + 2^(m-1)) for every
       // butterfly with e_j in {0, 2}, i.e. out(j, 0) in the class of y
       const uint32_t sym = (__builtin_popcount(rr) & 1u) ? so : se;
-      const uint32_t sel = rr | ((rr ^ 3u) << 16) | 0x0C000C00u;
-      cu32* tb = as_const(a.bmp);
-      asm volatile("" : "+s"(tb));   // per step: the table is re-read (scalar cache), not held in SGPRs
-      uint32_t kw[NW];
-      uint32_t zn = 0u;
-      k1b_acs<m, kSpec, XM>(a, tb, cur, rr, Dp, kw, sel, O8, zn);
-      // Eq. 5: step minimum 0 or 1
-      const uint32_t mu = (zn & 0x88888888u) == 0u;
-      const uint32_t mu8 = mu ? 0x11111111u : 0u;
-      O += mu;
-      O8 += mu8;
-      // P̂1 row of D_{t-1}
-      cur.fence(zn);                          // zn depends on the whole ACS
-      cur.template fence_keys<NW>(zn);
-      lp += cur.resolve(a, key, rr);          // Pd_plotter.py:115, T = P̂1
 #pragma unroll
       for (int v = 0; v < NW; ++v) key[v] = kw[v] - mu8;
       // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni

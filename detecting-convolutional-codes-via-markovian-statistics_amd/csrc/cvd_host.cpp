@@ -375,9 +375,9 @@ void build_hash(cvd_model& Mo) {
     throw std::length_error("explicit-path row table over 4 GiB (too many learned rows)");
   Mo.hcap = cap;
   int64_t fcap = 64;
-  while (fcap * 4 < Mo.n_rows) fcap <<= 1;   // >= 16 filter bits per row
+  while (fcap * 2 < Mo.n_rows) fcap <<= 1;   // >= 16 filter bits per row
   Mo.fcap = fcap;
-  Mo.h_filt.assign((size_t)fcap * 2, 0u);
+  Mo.h_filt.assign((size_t)fcap, 0u);
   Mo.h_key.assign((size_t)cap * nw, kEmptyKey);
   Mo.h_rsw = row_words(Mo.dec.n);
   Mo.h_row.assign((size_t)cap * Mo.h_rsw, 0u);
@@ -390,10 +390,7 @@ void build_hash(cvd_model& Mo) {
       for (int w = 0; w < nw; ++w) kw[w] = key_swap(kw[w]);   // device key layout
     uint32_t h1, h2;
     key_hash(kw.data(), nw, h1, h2);
-    uint32_t wi, lo, hi;
-    filter_probe(h1, h2, (uint32_t)(fcap - 1), wi, lo, hi);
-    Mo.h_filt[2 * (size_t)wi] |= lo;
-    Mo.h_filt[2 * (size_t)wi + 1] |= hi;
+    Mo.h_filt[(size_t)(h2 & (uint32_t)(fcap - 1))] |= filter_bits(filter_mix(h1, h2));
     uint64_t slot = h1 & (uint64_t)(cap - 1);
     int probe = 0;
     while (Mo.h_key[slot * nw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }

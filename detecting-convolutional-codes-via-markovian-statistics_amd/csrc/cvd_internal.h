@@ -31,7 +31,7 @@ struct cvd_model {
   int64_t hcap = 0;               // power of two, 0 = none
   int32_t max_probe = 0;
   std::vector<int64_t> row_next;  // [n_rows][2^n] row index of successor(row, r), -1 if not a row
-  std::vector<uint32_t> h_filt;   // [fcap][2] blocked Bloom filter words (filter_probe)
+  std::vector<uint32_t> h_filt;   // [fcap] blocked Bloom filter words (filter_bits)
   int64_t fcap = 0;               // filter words, power of two
   std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector, word 0 = kEmptyKey if empty
   int32_t h_rsw = 0;              // row record stride in dwords (row_words)

@@ -48,17 +48,15 @@ CVD_HD void key_hash(const unsigned* w, int nw, unsigned& h1, unsigned& h2) {
   h2 = (unsigned)q ^ (unsigned)(q >> 32);
 }
 
-// Blocked Bloom filter over the row keys (explicit path): one 64-bit word per
-// key, two bits in each 32-bit half.  A lookup of a state that is not a row
-// (most lookups at p >= 0.05 and for every H2 sequence) ends on this one
-// L2-resident load.  Word index from h2, bit positions from a third mix (the
-// shift counts are the low 5 bits of shifted copies, as v_lshlrev reads them).
-CVD_HD void filter_probe(unsigned h1, unsigned h2, unsigned fmask, unsigned& wi, unsigned& lo,
-                         unsigned& hi) {
-  wi = h2 & fmask;
-  const unsigned h3 = (h1 ^ rotl32(h2, 16)) * 0x9E3779B1u;
-  lo = (1u << (h3 & 31u)) | (1u << ((h3 >> 5) & 31u));
-  hi = (1u << ((h3 >> 10) & 31u)) | (1u << ((h3 >> 15) & 31u));
+// Blocked Bloom filter over the row keys (explicit path): one 32-bit word per
+// key, three bits in it.  A lookup of a state that is not a row (most lookups
+// at p >= 0.05 and for every H2 sequence) ends on this one L2-resident load.
+// Word index from h2, bit positions from a third mix (kept as one register,
+// filter_bits(), until the word arrives; shift counts are the low 5 bits of
+// shifted copies, as v_lshlrev reads them).
+CVD_HD unsigned filter_mix(unsigned h1, unsigned h2) { return (h1 ^ rotl32(h2, 16)) * 0x9E3779B1u; }
+CVD_HD unsigned filter_bits(unsigned h3) {
+  return (1u << (h3 & 31u)) | (1u << ((h3 >> 5) & 31u)) | (1u << ((h3 >> 10) & 31u));
 }
 
 // empty hash slot: key word 0 (a nibble-packed metric vector never has 15 in
