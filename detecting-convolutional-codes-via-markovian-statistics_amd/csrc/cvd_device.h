@@ -357,7 +357,7 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
   for (int j = 0; j < H; ++j) Dp[j] = E[j];
 }
 
-template <int m, bool kSpec, uint64_t XM>
+template <int m, bool kSpec, uint64_t XM, bool kTrace>
 __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
   constexpr int M = 1 << m, H = M / 2, NW = M / 8, R = 4;
   static_assert(m >= 3, "k1b kernel: 2^m >= 8 (whole key words)");
@@ -380,7 +380,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
 #pragma unroll
     for (int w = 0; w < NW; ++w) key[w] = 0u;
     uint32_t O = 0u, O8 = 0u;   // O8 = O * 0x11111111
-    if (a.trace) k1b_trace<m>(a.trace, 0, a.nseq, qwave + lane_id(), key);
+    if constexpr (kTrace) k1b_trace<m>(a.trace, 0, a.nseq, qwave + lane_id(), key);
     // Received words: word w of this sequence at rbase + (w/4)*cstride + w%4
     // (16-byte chunks, include/cvd.h).  Only the current word and the next are
     // held; the next is loaded when the current one starts, 12 steps before its
@@ -424,22 +424,21 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       } else {
         dh[0] = (key[0] ^ (key[0] >> 4)) & 0x0F0F0F0Fu;   // states s, s + 4 = nibbles 2i, 2i + 1
       }
-      uint32_t hx = 0u, se = 0u, so = 0u;
+      // pm: all ones when y has odd parity; the butterflies that decide the
+      // pair-swap test are those with out(j, 0) of y's parity
+      const uint32_t pm = 0u - (uint32_t)(__builtin_popcount(rr) & 1u);
+      uint32_t hx = 0u, sym = 0u;
 #pragma unroll
       for (int v = 0; v < NH; ++v) {
         hx |= dh[v];
-        se |= dh[v] & a.bfly_even[v];
-        so |= dh[v] & ~a.bfly_even[v];
+        sym |= dh[v] & (a.bfly_even[v] ^ pm);
       }
-      // D_t(y) == its pair swap iff D_{t-1}(j) == D_{t-1}(j + 2^(m-1)) for every
-      // butterfly with e_j in {0, 2}, i.e. out(j, 0) in the class of y
-      const uint32_t sym = (__builtin_popcount(rr) & 1u) ? so : se;
 #pragma unroll
       for (int v = 0; v < NW; ++v) key[v] = kw[v] - mu8;
       // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni
       const uint32_t c = 1u + (sym == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
       lr += s_lt[c];                          // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
-      if (a.trace) k1b_trace<m>(a.trace, t, a.nseq, qwave + lane_id(), key);
+      if constexpr (kTrace) k1b_trace<m>(a.trace, t, a.nseq, qwave + lane_id(), key);
       cur.prefetch(a, key, rn);
     };
 

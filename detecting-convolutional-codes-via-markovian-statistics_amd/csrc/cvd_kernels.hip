@@ -526,18 +526,18 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
 
 // k = 1, n = 2 butterfly detector with the branch metrics read from the
 // per-code table (cvd_device.h); hipRTC builds the code-specialised variant
-template <int m>
+template <int m, bool kTrace>
 __global__ __launch_bounds__(kBlock, kK1bWavesPerSimd) void detect_k1b_kernel(ExpArgs a) {
-  k1b_body<m, false, 0>(a);
+  k1b_body<m, false, 0, kTrace>(a);
 }
 
 using ExpKernel = void (*)(ExpArgs);
-ExpKernel pick_k1b(int m) {
+ExpKernel pick_k1b(int m, bool trace) {
   switch (m) {
-    case 3: return detect_k1b_kernel<3>;
-    case 4: return detect_k1b_kernel<4>;
-    case 5: return detect_k1b_kernel<5>;
-    case 6: return detect_k1b_kernel<6>;
+    case 3: return trace ? detect_k1b_kernel<3, true> : detect_k1b_kernel<3, false>;
+    case 4: return trace ? detect_k1b_kernel<4, true> : detect_k1b_kernel<4, false>;
+    case 5: return trace ? detect_k1b_kernel<5, true> : detect_k1b_kernel<5, false>;
+    case 6: return trace ? detect_k1b_kernel<6, true> : detect_k1b_kernel<6, false>;
   }
   return nullptr;
 }
@@ -628,12 +628,14 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
 
 // Kernel of the explicit path: the butterfly kernel when the code has standard
 // butterflies, else the orbit kernel (k = 1), else the generic one.
-static int select_explicit(const cvd_model& M, int variant, ExpKernel* kern, const uint32_t** bmp) {
+static int select_explicit(const cvd_model& M, int variant, ExpKernel* kern, const uint32_t** bmp,
+                           bool trace = false) {
   *kern = nullptr; *bmp = nullptr;
   if ((variant == cvd::kExplicitBest || variant == cvd::kExplicitButterfly) && M.k1b_ok) {
     *bmp = M.d_bfly;
-    if (variant == cvd::kExplicitBest && M.rtc_fn) return CVD_KERNEL_BUTTERFLY_RTC;
-    if (ExpKernel k = pick_k1b(M.dec.m)) { *kern = k; return CVD_KERNEL_BUTTERFLY; }
+    // the specialised kernel is built without the (test-only) trace path
+    if (variant == cvd::kExplicitBest && M.rtc_fn && !trace) return CVD_KERNEL_BUTTERFLY_RTC;
+    if (ExpKernel k = pick_k1b(M.dec.m, trace)) { *kern = k; return CVD_KERNEL_BUTTERFLY; }
   }
   if (variant != cvd::kExplicitGeneric && M.k1_ok)
     if (ExpKernel k = pick_k1(M.dec.m, M.dec.n)) { *kern = k; *bmp = M.d_bmk1; return CVD_KERNEL_ORBIT; }
@@ -653,7 +655,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
                                 void* stream, int variant) {
   ExpKernel kern = nullptr;
   const uint32_t* bmp = nullptr;
-  const int which = select_explicit(M, variant, &kern, &bmp);
+  const int which = select_explicit(M, variant, &kern, &bmp, d_trace != nullptr);
   if (which == CVD_KERNEL_NONE || !M.d_filt || !bmp) {
     set_error("explicit path: unsupported code shape (m,k,n)");
     return CVD_E_UNSUPPORTED;

@@ -49,7 +49,7 @@ std::string entry_source(int m, uint64_t xm) {
   char entry[256];
   std::snprintf(entry, sizeof(entry),
                 "\nextern \"C\" __global__ __launch_bounds__(cvd_dev::kBlock, cvd_dev::kK1bWavesPerSimd)\n"
-                "void cvd_k1b_spec(cvd_dev::ExpArgs a) { cvd_dev::k1b_body<%d, true, 0x%016llxull>(a); }\n",
+                "void cvd_k1b_spec(cvd_dev::ExpArgs a) { cvd_dev::k1b_body<%d, true, 0x%016llxull, false>(a); }\n",
                 m, (unsigned long long)xm);
   return entry;
 }
