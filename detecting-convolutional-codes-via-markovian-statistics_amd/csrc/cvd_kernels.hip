@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/cvd.h"
@@ -46,6 +47,8 @@ struct GenArgs {
   CodeDesc enc;
   uint32_t k0, k1, tag, thr_lo;
   int32_t thr_all, random_input;
+  int32_t hs;                     // gen_fast_kernel: history steps ceil(m / k)
+  uint32_t taps[kMaxN][2];        // gen_fast_kernel: shift set of output j on input phase r
   int64_t N, seq_base, seq_stride, pitch, q0, count;
   uint32_t* r;
 };
@@ -143,6 +146,178 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
     out4[w & 3] = word ^ nmask;
     if ((w & 3) == 3)
       *reinterpret_cast<uint4*>(a.r + chunk_index(w >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
+  }
+}
+
+// Bit-parallel generator for compile-time (k, n) with k <= 2 (every config
+// code): the same stream spec as gen_kernel, one SPW = 32/n step word at a time.
+//  * Encoder: out_j(t) = XOR_i g_{j,i}[0] u_i(t) ^ XOR_b c_j[b] s_b(t)
+//    (viterbi_markov.py:82-106 with x_i = u_i | s << 1), where s bit b is
+//    u_{b % k}(t - 1 - b / k) and c_j[b] = XOR_i g_{j,i}[1 + b].  Per input phase
+//    r the window W_r holds hs = ceil(m/k) history steps below the word's SPW
+//    input bits, so every term is one shift of a window: output stream j is the
+//    XOR of W_r >> sh over the host-built tap set taps[j][r] (bit sh), and the
+//    n streams are bit-interleaved into the word (step i in bits n*i .. n*i+n-1).
+//  * Noise: a group of GW words spans whole Philox blocks (GW = 1 for n = 2,
+//    2 for n = 3); each flip u < thr is the borrow of u - thr, shifted into the
+//    word's mask by one add-with-carry (two VOP2 per code bit), highest uniform
+//    first so uniform g0 + i lands on bit i.
+template <int n>
+__device__ __forceinline__ uint32_t spread_n(uint32_t x) {   // bit i -> bit n*i
+  if constexpr (n == 1) {
+    return x;
+  } else if constexpr (n == 2) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+  } else {
+    static_assert(n == 3, "spread_n: n in 1..3");
+    x &= 0x3FFu;
+    x = (x | (x << 16)) & 0xFF0000FFu;
+    x = (x | (x << 8)) & 0x0300F00Fu;
+    x = (x | (x << 4)) & 0x030C30C3u;
+    return (x | (x << 2)) & 0x09249249u;
+  }
+}
+
+__device__ __forceinline__ uint32_t even_bits(uint32_t x) {   // bit 2i -> bit i
+  x &= 0x55555555u;
+  x = (x | (x >> 1)) & 0x33333333u;
+  x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+  x = (x | (x >> 4)) & 0x00FF00FFu;
+  return (x | (x >> 8)) & 0x0000FFFFu;
+}
+
+__device__ __forceinline__ uint32_t shift_in_flip(uint32_t mask, uint32_t u, uint32_t thr) {
+  uint32_t t;
+  asm volatile("v_subrev_co_u32_e32 %0, vcc, %2, %3\n\t"
+               "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+               : "=&v"(t), "+v"(mask) : "s"(thr), "v"(u) : "vcc");
+  return mask;
+}
+
+template <int k, int n>
+__global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
+  constexpr int SPW = 32 / n, NBITS = SPW * n;
+  constexpr int GW = (NBITS % 4 == 0) ? 1 : (NBITS % 2 == 0) ? 2 : 4;
+  constexpr int NB = GW * NBITS / 4;          // Philox blocks per group
+  static_assert(k >= 1 && k <= 2 && SPW * k <= 32, "gen_fast_kernel: shape");
+  const int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (li >= a.count) return;
+  const int64_t q = a.q0 + li;
+  const uint64_t sid = (uint64_t)(a.seq_base + li * a.seq_stride);
+  const uint32_t slo = (uint32_t)sid, nhi = ctr_hi(sid, kKindNoise), ihi = ctr_hi(sid, kKindInput);
+  const int hs = a.hs;
+  const uint32_t hmask = (1u << hs) - 1u;
+  const int64_t nwords = (a.N + SPW - 1) / SPW;
+  const int64_t nw4 = (nwords + 3) & ~(int64_t)3;
+  int64_t iblk = -1;
+  U4 iv{0u, 0u, 0u, 0u};
+  auto input_word = [&](int64_t W) -> uint32_t {   // 32-bit word W of the input stream
+    if ((W >> 2) != iblk) {
+      iblk = W >> 2;
+      uint32_t k0 = a.k0, k1 = a.k1;
+      asm volatile("" : "+s"(k0), "+s"(k1));
+      iv = philox((uint32_t)iblk, slo, ihi, a.tag, k0, k1);
+    }
+    return u4_get(iv, (uint32_t)(W & 3));
+  };
+  // input bits [w*SPW*k, (w+1)*SPW*k) of the flat input stream, split by phase
+  auto word_inputs = [&](int64_t w, uint32_t (&U)[k]) {
+    uint32_t Fw = 0u;
+    if (a.random_input) {
+      const int64_t b0 = w * SPW * k;
+      const uint32_t off = (uint32_t)(b0 & 31);
+      const uint32_t lo = input_word(b0 >> 5);
+      const uint32_t hi = (off + SPW * k > 32u) ? input_word((b0 >> 5) + 1) : 0u;
+      Fw = off ? __builtin_amdgcn_alignbit(hi, lo, off) : lo;
+    }
+    if constexpr (k == 1) U[0] = Fw;
+    else { U[0] = even_bits(Fw); U[1] = even_bits(Fw >> 1); }
+#pragma unroll
+    for (int r = 0; r < k; ++r)
+      if constexpr (SPW < 32) U[r] &= (1u << SPW) - 1u;
+  };
+  // segment blockIdx.y of the sequence's 16-byte chunks: every word depends only
+  // on its own inputs and the hs input steps before it, so segments are
+  // independent (more waves in flight than one lane per sequence gives)
+  const int64_t nchunks = nw4 >> 2, seg = gridDim.y;
+  const int64_t c0 = nchunks * blockIdx.y / seg, c1 = nchunks * (blockIdx.y + 1) / seg;
+  uint32_t hist[k];
+#pragma unroll
+  for (int r = 0; r < k; ++r) hist[r] = 0u;   // encoder starts in state 0
+  if (c0 > 0 && 4 * c0 <= nwords) {
+    uint32_t Up[k];
+    word_inputs(4 * c0 - 1, Up);
+#pragma unroll
+    for (int r = 0; r < k; ++r) hist[r] = (Up[r] >> (SPW - hs)) & hmask;
+  }
+  for (int64_t w4 = 4 * c0; w4 < 4 * c1; w4 += 4) {
+    uint32_t out4[4];
+#pragma unroll
+    for (int g = 0; g < 4; g += GW) {
+      const int64_t wg = w4 + g;
+      uint32_t nm[GW];
+#pragma unroll
+      for (int e = 0; e < GW; ++e) nm[e] = 0u;
+      if (wg < nwords) {
+        if (a.thr_all) {
+#pragma unroll
+          for (int e = 0; e < GW; ++e) nm[e] = ~0u;
+        } else {
+          const uint32_t b0 = (uint32_t)(wg * NBITS / 4);
+#pragma unroll
+          for (int bb = NB - 1; bb >= 0; --bb) {
+            // launder the (uniform) key so its 10-round schedule is recomputed
+            // by scalar adds per call instead of being hoisted into SGPRs
+            uint32_t k0 = a.k0, k1 = a.k1;
+            asm volatile("" : "+s"(k0), "+s"(k1));
+            const U4 x = philox(b0 + (uint32_t)bb, slo, nhi, a.tag, k0, k1);
+            const uint32_t xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int e = 3; e >= 0; --e) {
+              const int ew = (4 * bb + e) / NBITS;
+              nm[ew] = shift_in_flip(nm[ew], xv[e], a.thr_lo);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < GW; ++e) {
+        const int64_t w = wg + e;
+        uint32_t word = 0u;
+        if (w < nwords) {
+          uint32_t U[k];
+          word_inputs(w, U);
+          uint32_t Wr[k];
+#pragma unroll
+          for (int r = 0; r < k; ++r) {
+            Wr[r] = (U[r] << hs) | hist[r];
+            hist[r] = (Wr[r] >> SPW) & hmask;
+          }
+#pragma unroll
+          for (int j = 0; j < n; ++j) {
+            uint32_t o = 0u;
+#pragma unroll
+            for (int r = 0; r < k; ++r) {
+              const uint32_t tm = a.taps[j][r];
+#pragma unroll
+              for (int sh = 0; sh <= kMaxM; ++sh)
+                if ((tm >> sh) & 1u) o ^= Wr[r] >> sh;
+            }
+            if constexpr (SPW < 32) o &= (1u << SPW) - 1u;
+            word |= spread_n<n>(o) << j;
+          }
+          word ^= nm[e];
+          const int64_t ns = a.N - w * SPW;           // steps in this word (last word: < SPW)
+          if (ns < SPW) word &= (1u << (n * ns)) - 1u;
+        }
+        out4[g + e] = word;
+      }
+    }
+    *reinterpret_cast<uint4*>(a.r + chunk_index(w4 >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
   }
 }
 
@@ -598,11 +773,33 @@ int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t
   a.random_input = random_input; a.N = N; a.seq_base = seq_base; a.seq_stride = seq_stride;
   a.pitch = pitch; a.q0 = q0; a.count = count; a.r = d_r;
   const unsigned grid = (unsigned)((count + kBlock - 1) / kBlock);
+  // bit-parallel generator: window taps per (output j, input phase r)
+  a.hs = (enc.m + enc.k - 1) / enc.k;
+  for (int j = 0; j < kMaxN; ++j) a.taps[j][0] = a.taps[j][1] = 0u;
+  for (int j = 0; j < enc.n; ++j)
+    for (int i = 0; i < enc.k; ++i) {
+      const uint32_t g = enc.gmask[j * enc.k + i];
+      if (g & 1u) a.taps[j][i] ^= 1u << a.hs;                     // u_i(t)
+      for (int b = 0; b < enc.m; ++b)                              // s bit b = u_{b%k}(t - 1 - b/k)
+        if ((g >> (1 + b)) & 1u) a.taps[j][b % enc.k] ^= 1u << (a.hs - 1 - b / enc.k);
+    }
+  const bool fast = !std::getenv("CVD_GEN_GENERIC") && enc.m <= kMaxM && a.hs + 32 / std::max(enc.n, 1) <= 32;
   auto kern = gen_kernel<0, 0>;
-  if (enc.k == 1 && enc.n == 2) kern = gen_kernel<1, 2>;
+  dim3 gdim(grid);
+  if (fast) {
+    // chunk segments per sequence: about 16 waves per SIMD (1024 SIMDs), >= 16 chunks each
+    const int64_t nchunks = (((N + 32 / enc.n - 1) / (32 / enc.n)) + 3) / 4;
+    const int64_t waves = (count + 63) / 64;
+    const int64_t seg = std::max<int64_t>(1, std::min<int64_t>((16 * 1024 + waves - 1) / waves, nchunks / 16));
+    gdim.y = (unsigned)std::min<int64_t>(seg, 65535);
+  }
+  if (fast && enc.k == 1 && enc.n == 2) kern = gen_fast_kernel<1, 2>;
+  else if (fast && enc.k == 1 && enc.n == 3) kern = gen_fast_kernel<1, 3>;
+  else if (fast && enc.k == 2 && enc.n == 3) kern = gen_fast_kernel<2, 3>;
+  else if (enc.k == 1 && enc.n == 2) kern = gen_kernel<1, 2>;
   else if (enc.k == 1 && enc.n == 3) kern = gen_kernel<1, 3>;
   else if (enc.k == 2 && enc.n == 3) kern = gen_kernel<2, 3>;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(kern, gdim, dim3(kBlock), 0, (hipStream_t)stream, a);
   HIP_CHECK(hipGetLastError());
   return CVD_OK;
 }

@@ -61,6 +61,29 @@ def test_generator_bit_exact(pkg, golden, dev, name, N, p, ri):
         np.testing.assert_array_equal(got[:, q], want)
 
 
+@pytest.mark.parametrize("name", ["m6_133_171", "r23_m4", "k1n3"])
+def test_fast_generator_equals_generic_long(pkg, golden, dev, name, monkeypatch):
+    """The bit-parallel generator (gen_fast_kernel) against the per-step generic
+    kernel at a long ragged N, and against the oracle on a few sequences."""
+    if name == "k1n3":
+        k, n, m, taps = 1, 3, 4, [[[1, 0, 1, 1, 1]], [[1, 1, 0, 1, 1]], [[1, 1, 1, 1, 1]]]
+    else:
+        z, meta = golden
+        k, n, m, taps = code_of(meta, name)
+    det = pkg.Detector(k, n, m, taps, device=0)
+    N, p, seed, count = 100_003, 0.07, 99, 300
+    tag = philox.grid_tag(N, p)
+    fast = det.generate(taps, N, p, seed, tag, 5, 2, count)
+    monkeypatch.setenv("CVD_GEN_GENERIC", "1")
+    generic = det.generate(taps, N, p, seed, tag, 5, 2, count)
+    monkeypatch.delenv("CVD_GEN_GENERIC")
+    assert torch.equal(fast, generic)
+    got = unpack_words(fast, n, N)
+    for q in (0, 131, count - 1):
+        want = R.received_stream(taps, m, k, n, N, p, seed, tag, 5 + 2 * q)
+        np.testing.assert_array_equal(got[:, q], want)
+
+
 # ───────────────────────────── metric trace ─────────────────────────────────
 
 @pytest.mark.parametrize("name", ["m2_75", "m3_demo", "r23_m4", "m6_133_171"])
