@@ -50,6 +50,9 @@ def parse():
                     help="P̂1 learning chain length for non-enumerable codes")
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--p", type=float, default=None, help="diagnostic: run one p instead of the sweep")
+    ap.add_argument("--overlap", type=int, default=-1,
+                    help="generate the next batch on a second stream while the detector runs "
+                         "(-1: auto = on for the table automaton, where it measured faster)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle port (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "detector_pmc.json"),
@@ -83,35 +86,71 @@ def main():
     info = models[p_grid[0]].info()
     # whole residency rounds: 4 waves/SIMD x 1024 SIMDs x 64 lanes = 262,144 sequences per round
     B = a.batch or {"m6": 262_144, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
-    r = det.stream_buffer(N, 2 * B)
+    # double-buffered pipeline: the generator fills buffer (s+1)%2 on its own
+    # stream while the detector reads buffer s%2 (both kernels of every timed
+    # step run inside the timed region)
+    if a.overlap < 0:
+        a.overlap = int(not info["kind"])
+    buf_bytes = det.words_per_seq(N) * 4 * 2 * B
+    if a.overlap and 2 * buf_bytes > (120 << 30):
+        a.overlap = 0                          # two batches would not leave HBM headroom
+    nbuf = 2 if a.overlap else 1
+    bufs = [det.stream_buffer(N, 2 * B) for _ in range(nbuf)]
     counts = torch.zeros((len(p_grid), 2), dtype=torch.int64, device=det.device)
-    stream = torch.cuda.current_stream()
+    dstream = torch.cuda.current_stream()
+    gstream = torch.cuda.Stream(device=det.device) if a.overlap else dstream
 
-    def step(s, ev=None):
+    def gen(s, ev=None):
         p = p_grid[s % len(p_grid)]
         tb = (s * world + rank) * B            # global trial ids of this rank's batch
         tag = pkg.grid_tag(N, p)
+        r = bufs[s % nbuf]
         if ev is not None:
-            ev[0].record(stream)
-        det.generate(g1, N, p, a.seed, tag, 2 * tb, 2, B, out=r, q0=0, pitch=2 * B)
-        det.generate(g2, N, p, a.seed, tag, 2 * tb + 1, 2, B, out=r, q0=B, pitch=2 * B)
+            ev[0].record(gstream)
+        det.generate(g1, N, p, a.seed, tag, 2 * tb, 2, B, out=r, q0=0, pitch=2 * B, stream=gstream)
+        det.generate(g2, N, p, a.seed, tag, 2 * tb + 1, 2, B, out=r, q0=B, pitch=2 * B, stream=gstream)
         if ev is not None:
-            ev[1].record(stream)
-        det.detect(models[p], r, N, 2 * B, B, counts=counts[s % len(p_grid)])
-        if ev is not None:
-            ev[2].record(stream)
+            ev[1].record(gstream)
 
-    for s in range(a.warmup):
-        step(10_000 + s)
+    def detect(s, ev=None):
+        p = p_grid[s % len(p_grid)]
+        if ev is not None:
+            ev[2].record(dstream)
+        det.detect(models[p], bufs[s % nbuf], N, 2 * B, B, counts=counts[s % len(p_grid)], stream=dstream)
+        if ev is not None:
+            ev[3].record(dstream)
+
+    def run(steps, base, events=None):
+        if not a.overlap:
+            for s in range(steps):
+                ev = events[s] if events else None
+                gen(base + s, ev)
+                detect(base + s, ev)
+            return
+        done = [torch.cuda.Event() for _ in range(steps)]
+        ready = [torch.cuda.Event() for _ in range(steps)]
+        gen(base, events[0] if events else None)
+        ready[0].record(gstream)
+        for s in range(steps):
+            dstream.wait_event(ready[s])
+            detect(base + s, events[s] if events else None)
+            done[s].record(dstream)
+            if s + 1 < steps:
+                if s >= 1:
+                    gstream.wait_event(done[s - 1])   # buffer (s+1)%2 was read by detect(s-1)
+                gen(base + s + 1, events[s + 1] if events else None)
+                ready[s + 1].record(gstream)
+        dstream.wait_stream(gstream)
+
+    run(a.warmup, 10_000)
     counts.zero_()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(a.steps)]
     t0 = time.perf_counter()
-    for s in range(a.steps):
-        step(s, events[s])
+    run(a.steps, 0, events)
     if dist:
         dist.all_reduce(counts)                # the one collective: success counts over RCCL
     torch.cuda.synchronize()
@@ -124,7 +163,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gen_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    det_each = [e[1].elapsed_time(e[2]) for e in events]
+    det_each = [e[2].elapsed_time(e[3]) for e in events]
     det_ms = float(np.mean(det_each))
 
     if rank != 0:
@@ -174,6 +213,7 @@ def main():
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
+                       "overlap": bool(a.overlap),
                        "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
                        "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
                        "detector_ms_steps": det_each,

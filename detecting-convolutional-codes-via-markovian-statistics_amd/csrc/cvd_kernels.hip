@@ -377,6 +377,84 @@ __global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
 
+// Enumerated automaton with the whole model LDS-resident (S < 4096 and
+// S*2^n*(8 + 2) + (2^n + 1)*8 bytes within the 160 KiB of a CU): records as
+// 16-bit next << 4 | c, log P̂1 as f64.  Per step one u16 and two f64 LDS
+// gathers; the only dependent chain is the u16 record (next state).  The
+// received words are read in 16-byte chunks one chunk ahead (64 or 40 steps
+// of lead), and full chunks run fully unrolled.
+template <int n>
+__device__ __forceinline__ void table16_word(uint32_t word, int ns, uint32_t& st, double& lp, double& lr,
+                                             const uint16_t* s_rec, const double* s_lp, const double* s_lt) {
+  constexpr uint32_t R = 1u << n;
+  for (int i = 0; i < ns; ++i) {
+    const uint32_t idx = st * R + (word & (R - 1u));
+    word >>= n;
+    const uint32_t e = s_rec[idx];
+    lp += s_lp[idx];                   // log P̂1[i, j]   (Pd_plotter.py:213)
+    lr += s_lt[e & 15u];               // log T_ref[i, j] = log(c / 2^n) (Pd_plotter.py:214)
+    st = e >> 4;
+  }
+}
+
+template <int n, int BS>
+__global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
+  constexpr int R = 1 << n, SPW = 32 / n;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int SR = (int)a.S * R;
+  double* s_lp = reinterpret_cast<double*>(smem);
+  double* s_lt = s_lp + SR;
+  uint16_t* s_rec = reinterpret_cast<uint16_t*>(s_lt + R + 1);
+  for (int i = threadIdx.x; i < SR; i += BS) {
+    s_lp[i] = a.logp1[i];
+    s_rec[i] = (uint16_t)a.rec[i];     // next < 4096: next << 4 | c fits 16 bits (host-checked)
+  }
+  for (int i = threadIdx.x; i <= R; i += BS) s_lt[i] = a.ltref[i];
+  __syncthreads();
+  const int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x;
+  const bool valid = q < a.nseq;
+  double lp = 0.0, lr = 0.0;
+  if (valid) {
+    const int64_t N = a.N, nwords = (N + SPW - 1) / SPW, nchunks = (nwords + 3) / 4;
+    const int64_t full = N / (4 * SPW);           // chunks whose 4 words are all full
+    const uint4* rc = reinterpret_cast<const uint4*>(a.r) + q;
+    const int64_t cs = a.nseq;                    // uint4 stride between chunks of one sequence
+    uint4 cur = make_uint4(0u, 0u, 0u, 0u), nxt = cur;
+    if (nchunks > 0) cur = rc[0];
+    if (nchunks > 1) nxt = rc[cs];
+    uint32_t st = 0;                              // index of D_0 = 0 (first BFS state)
+    for (int64_t c = 0; c < nchunks; ++c) {
+      const uint4 ch = cur;
+      cur = nxt;
+      if (c + 2 < nchunks) nxt = rc[(c + 2) * cs];
+      const uint32_t wv[4] = {ch.x, ch.y, ch.z, ch.w};
+      if (c < full) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t word = wv[e];
+#pragma unroll
+          for (int i = 0; i < SPW; ++i) {
+            const uint32_t idx = st * (uint32_t)R + (word & (uint32_t)(R - 1));
+            word >>= n;
+            const uint32_t rv = s_rec[idx];
+            lp += s_lp[idx];
+            lr += s_lt[rv & 15u];
+            st = rv >> 4;
+          }
+        }
+      } else {
+        for (int e = 0; e < 4; ++e) {
+          const int64_t t0 = (4 * c + e) * SPW;
+          if (t0 >= N) break;
+          table16_word<n>(wv[e], (int)min((int64_t)SPW, N - t0), st, lp, lr, s_rec, s_lp, s_lt);
+        }
+      }
+    }
+    if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+  }
+  count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
+}
+
 // pk16 minimum over L registers as a log-depth tree (independent ops issue back to back)
 template <int L>
 __device__ __forceinline__ us2 tree_min(const uint32_t (&A)[L]) {
@@ -814,6 +892,20 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
   a.S = M.S; a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   const size_t lds = (size_t)M.S * R * (sizeof(double) + sizeof(uint32_t)) + (R + 1) * sizeof(double);
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
+  // LDS-resident compact model (16-bit records): 1024-thread blocks when it
+  // takes most of a CU's 160 KiB, else 256-thread blocks
+  const size_t lds16 = (size_t)M.S * R * (sizeof(double) + sizeof(uint16_t)) + (R + 1) * sizeof(double);
+  if (M.S < 4096 && lds16 <= 160 * 1024 && (M.dec.n == 2 || M.dec.n == 3) && !std::getenv("CVD_TABLE_WIDE")) {
+    const bool big = lds16 > 40 * 1024;
+    const int bs = big ? 1024 : kBlock;
+    void (*kern)(TabArgs) = M.dec.n == 2 ? (big ? detect_table16_kernel<2, 1024> : detect_table16_kernel<2, kBlock>)
+                                         : (big ? detect_table16_kernel<3, 1024> : detect_table16_kernel<3, kBlock>);
+    if (lds16 > 64 * 1024)
+      HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds16));
+    hipLaunchKernelGGL(kern, dim3((unsigned)((nseq + bs - 1) / bs)), dim3(bs), lds16, (hipStream_t)stream, a);
+    HIP_CHECK(hipGetLastError());
+    return CVD_OK;
+  }
   if (lds <= 64 * 1024) {
     hipLaunchKernelGGL(detect_table_kernel<true>, dim3(grid), dim3(kBlock), lds, (hipStream_t)stream, a);
   } else {
