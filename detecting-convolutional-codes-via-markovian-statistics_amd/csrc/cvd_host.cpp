@@ -3,6 +3,14 @@
 // tables and the explicit-path hash.  None of this is the hot path (the trial
 // loop runs in cvd_kernels.hip); it is the analogue of the reference's table
 // construction (viterbi_markov.py:118-230, Pd_plotter.py:123-169).
+#include <chrono>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <tuple>
+#include <cstdlib>
+#include <exception>
+#include <cstdio>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -20,6 +28,20 @@ using namespace cvd;
 
 static thread_local std::string g_err;
 void cvd::set_error(const std::string& msg) { g_err = msg; }
+
+namespace {
+// CVD_SETUP_TIMING=1: phase times of cvd_model_create on stderr
+struct PhaseTimer {
+  bool on = std::getenv("CVD_SETUP_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  void mark(const char* what) {
+    if (!on) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[cvd setup] %-28s %8.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
+    t0 = t1;
+  }
+};
+}  // namespace
 
 #define CVD_TRY try {
 #define CVD_CATCH                                          \
@@ -99,6 +121,68 @@ inline void step_host(const Tabs& T, const uint8_t* D, uint32_t r, uint8_t* out)
   for (int i = 0; i < T.M; ++i) out[i] = (uint8_t)(best[i] - mn);
 }
 
+// The same step in predecessor form for k = 1 (next(s, u) = (2s + u) mod 2^m,
+// viterbi_markov.py:102-104): state x has predecessors x >> 1 and
+// (x >> 1) + 2^(m-1) with input x & 1.  bm[r][s][u] = popcount(out(s, u) ^ r).
+struct StepK1 {
+  int M;
+  std::vector<uint8_t> bm;   // [R][M][2]
+  explicit StepK1(const Tabs& T) : M(T.M), bm((size_t)T.R * T.M * 2) {
+    for (int r = 0; r < T.R; ++r)
+      for (int s = 0; s < T.M; ++s)
+        for (int u = 0; u < 2; ++u)
+          bm[((size_t)r * T.M + s) * 2 + u] = (uint8_t)__builtin_popcount((unsigned)(T.out[s * 2 + u] ^ r));
+  }
+  void operator()(const uint8_t* D, uint32_t r, uint8_t* out) const {
+    const uint8_t* b = bm.data() + (size_t)r * M * 2;
+    const int H = M / 2;
+    uint8_t mn = 255;
+    for (int x = 0; x < M; ++x) {
+      const int s0 = x >> 1, s1 = s0 + H, u = x & 1;
+      const int a = D[s0] + b[s0 * 2 + u], c = D[s1] + b[s1 * 2 + u];
+      const uint8_t v = (uint8_t)(a < c ? a : c);
+      out[x] = v;
+      mn = v < mn ? v : mn;
+    }
+    for (int x = 0; x < M; ++x) out[x] = (uint8_t)(out[x] - mn);
+  }
+};
+
+// Eq. 4-5 through the fastest form the code admits (identical results).
+struct HostStep {
+  const Tabs& T;
+  bool k1;
+  StepK1 s1;
+  explicit HostStep(const Tabs& t) : T(t), k1(t.k == 1), s1(t.k == 1 ? t : Tabs{1, 1, 1, 2, 2, 2, {0, 0, 0, 0}, {0, 0, 0, 0}}) {}
+  void operator()(const uint8_t* D, uint32_t r, uint8_t* out) const {
+    if (k1) s1(D, r, out);
+    else step_host(T, D, r, out);
+  }
+};
+
+// Run f(i) for i in [0, n) on up to `threads` std::threads (contiguous ranges).
+template <typename F>
+void parallel_for(int64_t n, F f) {
+  unsigned hw = std::thread::hardware_concurrency();
+  if (const char* e = std::getenv("CVD_HOST_THREADS")) hw = (unsigned)std::max(1, std::atoi(e));
+  const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({(int64_t)hw, (int64_t)32, n / 4096 + 1}));
+  if (nt == 1) { for (int64_t i = 0; i < n; ++i) f(i, 0); return; }
+  std::vector<std::thread> th;
+  std::exception_ptr err;
+  std::mutex mu;
+  for (int64_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      try {
+        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) f(i, (int)t);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu);
+        err = std::current_exception();
+      }
+    });
+  for (auto& x : th) x.join();
+  if (err) std::rethrow_exception(err);
+}
+
 // Open-addressing map from metric vectors (M bytes) to row indices.
 struct StateMap {
   int M;
@@ -107,6 +191,13 @@ struct StateMap {
   uint64_t mask = 0;
   int64_t count = 0;
   StateMap(int M_, std::vector<uint8_t>* st) : M(M_), store(st) { rehash(1024); }
+  // room for n keys without rehashing or moving the key store
+  void reserve(int64_t n) {
+    store->reserve((size_t)n * M);
+    uint64_t cap = mask + 1;
+    while ((uint64_t)n * 2 > cap) cap *= 2;
+    if (cap != mask + 1) rehash(cap);
+  }
   static uint64_t hb(const uint8_t* p, int M) {
     uint64_t h = 0x9E3779B97F4A7C15ull;
     for (int i = 0; i < M; i += 8) {
@@ -157,6 +248,7 @@ int bfs(const Tabs& T, int64_t cap, std::vector<uint8_t>& states, std::vector<in
   next.clear();
   StateMap map(T.M, &states);
   std::vector<uint8_t> zero((size_t)T.M, 0), nb((size_t)T.M);
+  const HostStep step(T);
   bool ins;
   map.insert(zero.data(), ins);
   int64_t head = 0;
@@ -167,7 +259,7 @@ int bfs(const Tabs& T, int64_t cap, std::vector<uint8_t>& states, std::vector<in
     for (int i = 0; i < T.R; ++i) {
       uint32_t r = 0;
       for (int j = 0; j < T.n; ++j) r |= ((uint32_t)(i >> (T.n - 1 - j)) & 1u) << j;
-      step_host(T, states.data() + (size_t)head * T.M, r, nb.data());
+      step(states.data() + (size_t)head * T.M, r, nb.data());
       int64_t j = map.insert(nb.data(), ins);
       if (map.count > cap) { S = map.count; return CVD_E_CAPACITY; }
       next[(size_t)head * T.R + r] = (int32_t)j;
@@ -383,13 +475,17 @@ void build_hash(cvd_model& Mo) {
   Mo.h_row.assign((size_t)cap * Mo.h_rsw, 0u);
   Mo.max_probe = 0;
   std::vector<int64_t> slot_of((size_t)Mo.n_rows);
-  std::vector<uint32_t> kw((size_t)nw);
-  for (int64_t i = 0; i < Mo.n_rows; ++i) {
-    pack_nibbles(Mo.keys.data() + (size_t)i * M, M, kw.data());
+  std::vector<uint32_t> kws((size_t)Mo.n_rows * nw), h1s((size_t)Mo.n_rows), h2s((size_t)Mo.n_rows);
+  parallel_for(Mo.n_rows, [&](int64_t i, int) {
+    uint32_t* kw = kws.data() + (size_t)i * nw;
+    pack_nibbles(Mo.keys.data() + (size_t)i * M, M, kw);
     if (M >= 8)
       for (int w = 0; w < nw; ++w) kw[w] = key_swap(kw[w]);   // device key layout
-    uint32_t h1, h2;
-    key_hash(kw.data(), nw, h1, h2);
+    key_hash(kw, nw, h1s[(size_t)i], h2s[(size_t)i]);
+  });
+  for (int64_t i = 0; i < Mo.n_rows; ++i) {
+    const uint32_t* kw = kws.data() + (size_t)i * nw;
+    const uint32_t h1 = h1s[(size_t)i], h2 = h2s[(size_t)i];
     Mo.h_filt[(size_t)(h2 & (uint32_t)(fcap - 1))] |= filter_bits(filter_mix(h1, h2));
     uint64_t slot = h1 & (uint64_t)(cap - 1);
     int probe = 0;
@@ -398,14 +494,14 @@ void build_hash(cvd_model& Mo) {
     for (int w = 0; w < nw; ++w) Mo.h_key[slot * nw + w] = kw[w];
     slot_of[(size_t)i] = (int64_t)slot;
   }
-  for (int64_t i = 0; i < Mo.n_rows; ++i) {
+  parallel_for(Mo.n_rows, [&](int64_t i, int) {
     uint32_t* rw = Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw;
     std::memcpy(rw, Mo.logp1.data() + (size_t)i * R, sizeof(double) * R);
     for (int r = 0; r < R; ++r) {
       const int64_t j = Mo.row_next[(size_t)i * R + r];
       rw[2 * R + r] = (uint32_t)(j >= 0 ? (int32_t)slot_of[(size_t)j] : -1);
     }
-  }
+  });
   Mo.slot0 = (int32_t)slot_of[0];   // D_0 = 0 is row 0 in both model kinds
 }
 
@@ -511,11 +607,30 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
   for (int c = 0; c <= R; ++c) Mo->ltref[c] = ltref_value(c, R);
   const uint64_t seed = prm->seed;
 
+  PhaseTimer pt;
   std::vector<uint8_t> states;
   std::vector<int32_t> next;
   int64_t S = 0;
   const int64_t cap = prm->enum_cap > 0 ? prm->enum_cap : 0;
-  rc = cap > 0 ? bfs(T, cap, states, next, S) : CVD_E_CAPACITY;
+  // a code whose BFS outgrew the cap once always will: remember it per
+  // process (the model is built once per p, the BFS outcome is p-independent)
+  static std::mutex bfs_mu;
+  static std::map<std::tuple<int, int, int, std::vector<uint32_t>>, int64_t> bfs_too_big;   // -> largest cap tried
+  const auto ckey = std::make_tuple(T.m, T.k, T.n,
+                                    std::vector<uint32_t>(Mo->dec.gmask, Mo->dec.gmask + T.n * T.k));
+  bool known_big = false;
+  {
+    std::lock_guard<std::mutex> lk(bfs_mu);
+    auto it = bfs_too_big.find(ckey);
+    known_big = it != bfs_too_big.end() && it->second >= cap;
+  }
+  rc = (cap > 0 && !known_big) ? bfs(T, cap, states, next, S) : CVD_E_CAPACITY;
+  if (rc == CVD_E_CAPACITY && cap > 0 && !known_big) {
+    std::lock_guard<std::mutex> lk(bfs_mu);
+    int64_t& c = bfs_too_big[ckey];
+    c = std::max(c, cap);
+  }
+  pt.mark("bfs");
   std::unordered_map<int64_t, double> memo;
 
   if (rc == CVD_OK) {
@@ -570,8 +685,10 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
     Mo->learn_len_eff = L;
     std::vector<uint8_t> keys;
     StateMap map(M, &keys);
+    map.reserve(std::min<int64_t>(L + 1, (int64_t)1 << 26));
     std::vector<int64_t> cnt;
     std::vector<uint8_t> D((size_t)M, 0), Dn((size_t)M);
+    const HostStep step(T);
     bool ins;
     int64_t i = map.insert(D.data(), ins);
     cnt.resize((size_t)R, 0);
@@ -579,26 +696,32 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
     for (int64_t t = 0; t < L; ++t) {
       const uint32_t r = hs.next_word(t);
       if (t >= prm->learn_burn) cnt[(size_t)i * R + r]++;
-      step_host(T, D.data(), r, Dn.data());
+      step(D.data(), r, Dn.data());
       int64_t j = map.insert(Dn.data(), ins);
       if (ins) cnt.resize((size_t)map.count * R, 0);
       std::swap(D, Dn);
       i = j;
     }
+    pt.mark("chain");
     S = map.count;
     Mo->S = S;
     Mo->n_rows = S;
     Mo->logp1.assign((size_t)S * R, 0.0);
-    std::vector<int64_t> succ((size_t)R);
-    for (int64_t s = 0; s < S; ++s) {
+    Mo->row_next.assign((size_t)S * R, -1);
+    // successors and P̂1 rows: independent per row (read-only map), on host threads
+    std::vector<std::unordered_map<int64_t, double>> memos(32);
+    parallel_for(S, [&](int64_t s, int tid) {
+      uint8_t nb[256];
+      int64_t succ[16];
       for (int r = 0; r < R; ++r) {
-        step_host(T, keys.data() + (size_t)s * M, (uint32_t)r, Dn.data());
-        succ[r] = map.find(Dn.data());
+        step(keys.data() + (size_t)s * M, (uint32_t)r, nb);
+        succ[r] = map.find(nb);
       }
-      for (int r = 0; r < R; ++r) Mo->row_next.push_back(succ[r]);
-      p1_row(S, prm->laplace, memo, succ.data(), cnt.data() + (size_t)s * R, R,
+      for (int r = 0; r < R; ++r) Mo->row_next[(size_t)s * R + r] = succ[r];
+      p1_row(S, prm->laplace, memos[(size_t)tid], succ, cnt.data() + (size_t)s * R, R,
              Mo->logp1.data() + (size_t)s * R);
-    }
+    });
+    pt.mark("successors + P1 rows");
     Mo->keys = std::move(keys);
     std::vector<int64_t> none((size_t)R, -1), zc((size_t)R, 0);
     std::vector<double> lp((size_t)R);
@@ -610,6 +733,7 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
   if (explicit_supported(T.m, T.k, T.n)) {
     build_hash(*Mo);
     build_bmp(*Mo, T);
+    pt.mark("row table");
   }
   *out = Mo.release();
   return CVD_OK;
