@@ -11,3 +11,8 @@ from .detector import (  # noqa: F401
     enumerate_markov_states_allzero, build_trellis, branch_output_and_next_state,
     viterbi_metric_step, simulate_markov_sequence, log_likelihood_ratio, grid_tag, LEARN_TAG,
 )
+from .parity import (  # noqa: F401
+    parse_poly_token, build_parity_system, nullspace_mod2, parity_vector_to_equation, parity_vectors,
+    template_of, default_template, parity_detect, parity_satisfaction_fraction, parity_detector,
+    parity_experiment,
+)

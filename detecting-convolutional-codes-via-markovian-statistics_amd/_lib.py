@@ -12,7 +12,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5
 
@@ -79,6 +79,9 @@ EXPORTS = {
                                   ctypes.c_double, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_int32, ctypes.c_void_p]),
+    "cvd_parity_detect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _lib = None

@@ -14,6 +14,8 @@
  *   Pd_plotter.py:106-116     log_prob_sequence                                    cvd_detect (per-sequence sums)
  *   Pd_plotter.py:198-233     trial loop, decision, Pd/Pc counting                 cvd_detect (counts) / cvd_mc_run
  *   (none: the reference is single-process)                                        counts reduced by the caller over RCCL
+ *   comp_parity.py:90-128     parity_satisfaction_fraction / parity_detector       cvd_parity_detect
+ *                             (parity-template baseline)
  *
  * Conventions:
  *   - every function returns 0 on success, a negative CVD_E* code on error;
@@ -32,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 2
+#define CVD_ABI_VERSION 3
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -151,6 +153,19 @@ int64_t cvd_mc_workspace_bytes(const cvd_code* enc1, int64_t N, int64_t batch);
 int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2,
                double p, int64_t N, uint64_t seed, int64_t trial_begin, int64_t trial_end,
                int64_t batch, void* d_work, int64_t* d_counts, int32_t path, void* stream);
+
+/* ---- parity-template baseline (comp_parity.py, parity_eqn_check.py) --------
+ * Per sequence q of a received-word buffer (pitch = nseq, layout as above):
+ *   sat = #{t in [max_s, N) : XOR_{(j,s) in terms} y_j[t - s] == 0}
+ * with y_j[t] = bit j of step t (comp_parity.py:90-117: anchors from the
+ * template's largest delay max_s), P̂ = sat / (N - max_s), 0.0 without anchors.
+ * Sequences q < n_h1 succeed iff P̂ >= gamma (decide H1), the rest iff P̂ < gamma
+ * (comp_parity.py:120-128); d_counts[2] accumulated as in cvd_detect.
+ * terms: [n_terms][2] (output j, delay s), 1 <= n <= 3, 1 <= n_terms <= 64,
+ * 0 <= s <= 64 - floor(32/n).  d_sat (nullable): [nseq] int32 satisfied counts. */
+int cvd_parity_detect(const uint32_t* d_r, int32_t n, int64_t N, int64_t nseq, int64_t n_h1,
+                      const int32_t* terms, int32_t n_terms, double gamma, int32_t* d_sat,
+                      int64_t* d_counts, void* stream);
 
 #ifdef __cplusplus
 }
