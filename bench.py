@@ -50,6 +50,10 @@ def parse():
                     help="P̂1 learning chain length for non-enumerable codes")
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--p", type=float, default=None, help="diagnostic: run one p instead of the sweep")
+    ap.add_argument("--detector", default="markov", choices=["markov", "parity"],
+                    help="markov: the relative-Viterbi-metric detector (headline); parity: the "
+                         "parity-template baseline of comp_parity.py on the same streams")
+    ap.add_argument("--gamma", type=float, default=0.6, help="parity baseline threshold (comp_parity.py:151)")
     ap.add_argument("--overlap", type=int, default=-1,
                     help="generate the next batch on a second stream while the detector runs "
                          "(-1: auto = on for the table automaton, where it measured faster)")
@@ -82,8 +86,14 @@ def main():
     det = pkg.Detector(k, n, m, cc["gen1"], device=local)
     g1 = pkg.Code(cc["gen1"], m, k, n)
     g2 = pkg.Code(cc["gen2"], m, k, n)
-    models = {p: det.model(p, a.learn_len if m == 6 else None, 200, 1.0, a.seed) for p in p_grid}
-    info = models[p_grid[0]].info()
+    parity = a.detector == "parity"
+    if parity:
+        # parity-template baseline (comp_parity.py): template of G1, no learned model
+        tpl = pkg.default_template(cc["gen1"], m)
+        models, info = {}, {"kind": 0, "explicit_kernel": 0, "learn_len_eff": 0, "n_rows": 0}
+    else:
+        models = {p: det.model(p, a.learn_len if m == 6 else None, 200, 1.0, a.seed) for p in p_grid}
+        info = models[p_grid[0]].info()
     # whole residency rounds: 4 waves/SIMD x 1024 SIMDs x 64 lanes = 262,144 sequences per round
     B = a.batch or {"m6": 262_144, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
     # double-buffered pipeline: the generator fills buffer (s+1)%2 on its own
@@ -116,7 +126,11 @@ def main():
         p = p_grid[s % len(p_grid)]
         if ev is not None:
             ev[2].record(dstream)
-        det.detect(models[p], bufs[s % nbuf], N, 2 * B, B, counts=counts[s % len(p_grid)], stream=dstream)
+        if parity:
+            pkg.parity_detect(bufs[s % nbuf], n, N, 2 * B, B, tpl, a.gamma, counts=counts[s % len(p_grid)],
+                              stream=dstream)
+        else:
+            det.detect(models[p], bufs[s % nbuf], N, 2 * B, B, counts=counts[s % len(p_grid)], stream=dstream)
         if ev is not None:
             ev[3].record(dstream)
 
@@ -180,7 +194,8 @@ def main():
     if a.pmc_traffic and os.path.exists(a.pmc_traffic):
         with open(a.pmc_traffic) as f:
             pmc = json.load(f)
-        if (pmc.get("config"), pmc.get("batch"), pmc.get("N")) == (a.config, B, N):
+        if (pmc.get("config"), pmc.get("batch"), pmc.get("N"), pmc.get("detector", "markov")) == \
+                (a.config, B, N, a.detector):
             traffic = pmc.get("detector_fetch_bytes_per_launch")
             valu = {k: pmc.get(k) for k in ("VALU_insts_per_wave_step", "valu_issue_frac_est", "kernel")}
             traffic_src = os.path.relpath(a.pmc_traffic, ROOT) + " (rocprofv3 FETCH_SIZE x1024 x2, gfx950 correction)"
@@ -189,7 +204,8 @@ def main():
                       "h1_successes": int(c[i, 0]), "h2_successes": int(c[i, 1])}
              for i, p in enumerate(p_grid)}
     out = {
-        "metric": METRIC if a.config == "m6" else f"MC trials/sec ({a.config}, N={N})",
+        "metric": (METRIC if a.config == "m6" and not parity
+                   else f"MC trials/sec ({a.config}, N={N}{', parity-template baseline' if parity else ''})"),
         "value": value,
         "unit": "trials/s",
         "n_gpus": world,
@@ -208,7 +224,8 @@ def main():
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": (pkg.KERNEL_NAMES[info["explicit_kernel"]] if info["kind"]
+                     "kernel": ("parity_kernel (parity-template baseline, cvd_parity.hip)" if parity
+                                else pkg.KERNEL_NAMES[info["explicit_kernel"]] if info["kind"]
                                 else "detect_table_kernel (enumerated state automaton)"),
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms},
@@ -221,7 +238,7 @@ def main():
                        "valu_bound": valu,
                        "per_p": per_p},
     }
-    if a.cpu_baseline and world == 1:
+    if a.cpu_baseline and world == 1 and not parity:
         out["cpu_baseline"] = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds)
     print(json.dumps(out), flush=True)
     if dist:

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <string>
+#include <type_traits>
 
 #include "../../include/cvd.h"
 #include "cvd_internal.h"
@@ -22,7 +23,7 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kMaxTerms = 64;
+constexpr int kMaxTerms = 32;   // per output stream (n = 3) / in total (n <= 2)
 constexpr int kMaxOut = 3;
 
 struct ParArgs {
@@ -30,38 +31,35 @@ struct ParArgs {
   int64_t N, nseq, n_h1;
   int64_t first;               // first anchor: max delay of the template
   double gamma;
-  uint32_t sh[kMaxTerms];      // window shift of each term: 64 - SPW - s, grouped by output
-  int32_t tbeg[kMaxOut + 1];   // terms of output j: [tbeg[j], tbeg[j+1])
+  // n <= 2 (interleaved words): a term reads stream bit (n*t0 + n*i) - o,
+  // o = n*s - j, as alignbit(hi, lo, sh) of word pair g: 0 = (cur, prev),
+  // 1 = (prev, prev2), 2 = (cur, cur) for o <= 0; sh[g][k], cnt[g] terms.
+  // n = 3 (de-interleaved): term k of output j shifts its 64-bit window by sh[j][k]
+  uint32_t sh[kMaxOut][kMaxTerms];
+  uint32_t mk[kMaxOut][kMaxTerms];   // n <= 2: all ones for a term, 0 for padding
+  int32_t cnt[kMaxOut];
   int32_t* sat;
   int64_t* counts;
 };
 
-// bits n*i + j of x -> bit i (output j of step i)
-template <int n>
-__device__ __forceinline__ uint32_t output_bits(uint32_t x, int j) {
-  x >>= j;
-  if constexpr (n == 1) {
-    return x;
-  } else if constexpr (n == 2) {
-    x &= 0x55555555u;
-    x = (x | (x >> 1)) & 0x33333333u;
-    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
-    x = (x | (x >> 4)) & 0x00FF00FFu;
-    return (x | (x >> 8)) & 0x0000FFFFu;
-  } else {
-    static_assert(n == 3, "parity kernel: n in 1..3");
-    x &= 0x09249249u;
-    x = (x | (x >> 2)) & 0x030C30C3u;
-    x = (x | (x >> 4)) & 0x0300F00Fu;
-    x = (x | (x >> 8)) & 0xFF0000FFu;
-    return (x | (x >> 16)) & 0x000003FFu;
-  }
+// bits 3i + j of x -> bit i (output j of step i)
+__device__ __forceinline__ uint32_t output_bits3(uint32_t x, int j) {
+  x = (x >> j) & 0x09249249u;
+  x = (x | (x >> 2)) & 0x030C30C3u;
+  x = (x | (x >> 4)) & 0x0300F00Fu;
+  x = (x | (x >> 8)) & 0xFF0000FFu;
+  return (x | (x >> 16)) & 0x000003FFu;
 }
 
-template <int n>
+// n <= 2: T0 / T1 / T2 term slots of the word pairs (cur, prev) / (prev, prev2) /
+// (cur, cur), unrolled with compile-time indices so the shift amounts and masks
+// stay in SGPRs for the whole kernel; a padding slot has mask 0 (one bitop3
+// P ^ (x & mask) per slot).  n = 3: uniform runtime loops.
+template <int n, int T0 = 0, int T1 = 0, int T2 = 0>
 __global__ __launch_bounds__(kBlock) void parity_kernel(ParArgs a) {
   constexpr int SPW = 32 / n;
-  constexpr uint32_t LOW = SPW == 32 ? ~0u : (1u << SPW) - 1u;
+  // anchor bits of a word: bit n*i for step i (n <= 2, interleaved), bit i (n = 3)
+  constexpr uint32_t LANES = n == 1 ? ~0u : n == 2 ? 0x55555555u : 0x3FFu;
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = q < a.nseq;
   int64_t sat = 0;
@@ -70,32 +68,62 @@ __global__ __launch_bounds__(kBlock) void parity_kernel(ParArgs a) {
     const int64_t nwords = (N + SPW - 1) / SPW, nchunks = (nwords + 3) / 4;
     const uint4* rc = reinterpret_cast<const uint4*>(a.r) + q;
     const int64_t cs = a.nseq;   // uint4 stride between chunks of one sequence
-    uint4 cur = make_uint4(0u, 0u, 0u, 0u), nxt = cur;
-    if (nchunks > 0) cur = rc[0];
-    if (nchunks > 1) nxt = rc[cs];
-    uint64_t win[n];
+    uint4 c0 = make_uint4(0u, 0u, 0u, 0u), c1 = c0, c2 = c0;
+    if (nchunks > 0) c0 = rc[0];
+    if (nchunks > 1) c1 = rc[cs];
+    if (nchunks > 2) c2 = rc[2 * cs];
+    uint32_t prev = 0u, prev2 = 0u;   // n <= 2: the two words before the current one
+    uint64_t win[n == 3 ? 3 : 1];     // n = 3: per-output windows, bit 64 - SPW + i = y_j[t0 + i]
 #pragma unroll
-    for (int j = 0; j < n; ++j) win[j] = 0ull;
-    for (int64_t c = 0; c < nchunks; ++c) {
-      const uint4 ch = cur;
-      cur = nxt;
-      if (c + 2 < nchunks) nxt = rc[(c + 2) * cs];
+    for (int j = 0; j < (n == 3 ? 3 : 1); ++j) win[j] = 0ull;
+    // one chunk (4 words); kEdge: mask the anchors outside [first, N)
+    auto chunk = [&](const uint4& ch, int64_t c, auto edge) {
+      constexpr bool kEdge = decltype(edge)::value;
       const uint32_t wv[4] = {ch.x, ch.y, ch.z, ch.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t t0 = (4 * c + e) * SPW;
+        const uint32_t cur = wv[e];
         uint32_t P = 0u;
+        if constexpr (n <= 2) {
 #pragma unroll
-        for (int j = 0; j < n; ++j) {
-          win[j] = (win[j] >> SPW) | ((uint64_t)output_bits<n>(wv[e], j) << (64 - SPW));
-          for (int k = a.tbeg[j]; k < a.tbeg[j + 1]; ++k) P ^= (uint32_t)(win[j] >> a.sh[k]);
+          for (int k = 0; k < T0; ++k) P ^= __builtin_amdgcn_alignbit(cur, prev, a.sh[0][k]) & a.mk[0][k];
+#pragma unroll
+          for (int k = 0; k < T1; ++k) P ^= __builtin_amdgcn_alignbit(prev, prev2, a.sh[1][k]) & a.mk[1][k];
+#pragma unroll
+          for (int k = 0; k < T2; ++k) P ^= __builtin_amdgcn_alignbit(cur, cur, a.sh[2][k]) & a.mk[2][k];
+          prev2 = prev;
+          prev = cur;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            win[j] = (win[j] >> SPW) | ((uint64_t)output_bits3(cur, j) << (64 - SPW));
+#pragma nounroll
+            for (int k = 0; k < a.cnt[j]; ++k) P ^= (uint32_t)(win[j] >> a.sh[j][k]);
+          }
         }
-        // anchors of this word: first <= t0 + i < N
-        uint32_t vm = LOW;
-        if (t0 < a.first) vm = a.first - t0 >= SPW ? 0u : vm & ~((1u << (a.first - t0)) - 1u);
-        if (t0 + SPW > N) vm = t0 >= N ? 0u : vm & ((1u << (N - t0)) - 1u);
+        uint32_t vm = LANES;
+        if constexpr (kEdge) {
+          // anchors of this word: first <= t0 + i < N
+          const int64_t t0 = (4 * c + e) * SPW;
+          const int64_t lo_i = a.first > t0 ? a.first - t0 : 0;
+          const int64_t hi_i = N - t0 < SPW ? N - t0 : SPW;
+          vm = 0u;
+          for (int64_t i = lo_i; i < hi_i; ++i) vm |= 1u << (uint32_t)((n <= 2 ? n : 1) * i);
+        }
         sat += __builtin_popcount(~P & vm);
       }
+    };
+    // chunks [0, head) may hold steps before the first anchor, chunks from
+    // `tail` on steps at or after N; the body needs no masking
+    constexpr int64_t CS = 4 * SPW;   // steps per chunk
+    const int64_t head = (a.first + CS - 1) / CS, tail = N / CS;
+    for (int64_t c = 0; c < nchunks; ++c) {
+      const uint4 ch = c0;
+      c0 = c1;
+      c1 = c2;
+      if (c + 3 < nchunks) c2 = rc[(c + 3) * cs];
+      if (c < head || c >= tail) chunk(ch, c, std::true_type{});
+      else chunk(ch, c, std::false_type{});
     }
     if (a.sat) a.sat[q] = (int32_t)sat;
   }
@@ -126,8 +154,8 @@ extern "C" int cvd_parity_detect(const uint32_t* d_r, int32_t n, int64_t N, int6
                                  const int32_t* terms, int32_t n_terms, double gamma, int32_t* d_sat,
                                  int64_t* d_counts, void* stream) {
   if (n < 1 || n > kMaxOut || N < 0 || nseq < 0 || n_h1 < 0 || n_h1 > nseq || !d_counts ||
-      (!d_r && N > 0 && nseq > 0) || n_terms < 1 || n_terms > kMaxTerms || !terms) {
-    cvd::set_error("bad parity_detect arguments (1 <= n <= 3, 1 <= n_terms <= 64)");
+      (!d_r && N > 0 && nseq > 0) || n_terms < 1 || n_terms > kMaxOut * kMaxTerms || !terms) {
+    cvd::set_error("bad parity_detect arguments (1 <= n <= 3, 1 <= n_terms <= 96)");
     return CVD_E_INVALID;
   }
   if (N > 0x7FFFFFFF) { cvd::set_error("parity_detect: N must fit 31 bits"); return CVD_E_INVALID; }
@@ -135,25 +163,49 @@ extern "C" int cvd_parity_detect(const uint32_t* d_r, int32_t n, int64_t N, int6
   ParArgs a{};
   a.r = d_r; a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.gamma = gamma; a.sat = d_sat; a.counts = d_counts;
   int64_t first = 0;
-  int k = 0;
-  for (int j = 0; j < n; ++j) {
-    a.tbeg[j] = k;
-    for (int e = 0; e < n_terms; ++e) {
-      const int tj = terms[2 * e], ts = terms[2 * e + 1];
-      if (tj < 0 || tj >= n || ts < 0 || ts > 64 - spw) {
-        cvd::set_error("parity_detect: term (j, s) needs 0 <= j < n and 0 <= s <= 64 - 32/n");
-        return CVD_E_INVALID;
-      }
-      if (tj != j) continue;
-      a.sh[k++] = (uint32_t)(64 - spw - ts);
-      first = std::max<int64_t>(first, ts);
+  for (int e = 0; e < n_terms; ++e) {
+    const int tj = terms[2 * e], ts = terms[2 * e + 1];
+    const int smax = n <= 2 ? (64 + tj) / n : 64 - spw;   // n <= 2: o = n*s - j <= 64
+    if (tj < 0 || tj >= n || ts < 0 || ts > smax) {
+      cvd::set_error("parity_detect: term (j, s) needs 0 <= j < n and n*s - j <= 64 (n <= 2) / s <= 54 (n = 3)");
+      return CVD_E_INVALID;
+    }
+    first = std::max<int64_t>(first, ts);
+    if (n <= 2) {
+      const int o = n * ts - tj;   // bits back from the anchor bit n*i
+      const int g = o <= 0 ? 2 : o <= 32 ? 0 : 1;
+      const uint32_t sh = o <= 0 ? (uint32_t)(-o) : o <= 32 ? (uint32_t)(32 - o) : (uint32_t)(64 - o);
+      int& c = a.cnt[g];
+      if (c >= kMaxTerms) { cvd::set_error("parity_detect: more than 32 terms per word pair"); return CVD_E_INVALID; }
+      a.mk[g][c] = ~0u;
+      a.sh[g][c++] = sh;
+    } else {
+      int& c = a.cnt[tj];
+      if (c >= kMaxTerms) { cvd::set_error("parity_detect: more than 32 terms per output"); return CVD_E_INVALID; }
+      a.sh[tj][c++] = (uint32_t)(64 - spw - ts);
     }
   }
-  for (int j = n; j <= kMaxOut; ++j) a.tbeg[j] = k;
   a.first = first;
   if (nseq == 0) return CVD_OK;
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
-  void (*kern)(ParArgs) = n == 1 ? parity_kernel<1> : n == 2 ? parity_kernel<2> : parity_kernel<3>;
+  void (*kern)(ParArgs) = parity_kernel<3>;
+  if (n <= 2) {
+    // padded slot counts: T0 in {4, 8, 16, 32}, T1 in {0, 32}, T2 = 2
+    const int c0 = a.cnt[0], c1 = a.cnt[1];
+    const int T0 = c0 <= 4 ? 4 : c0 <= 8 ? 8 : c0 <= 16 ? 16 : 32;
+    using K = void (*)(ParArgs);
+    static const K k1[2][4] = {{parity_kernel<1, 4, 0, 2>, parity_kernel<1, 8, 0, 2>, parity_kernel<1, 16, 0, 2>,
+                                parity_kernel<1, 32, 0, 2>},
+                               {parity_kernel<1, 4, 32, 2>, parity_kernel<1, 8, 32, 2>, parity_kernel<1, 16, 32, 2>,
+                                parity_kernel<1, 32, 32, 2>}};
+    static const K k2[2][4] = {{parity_kernel<2, 4, 0, 2>, parity_kernel<2, 8, 0, 2>, parity_kernel<2, 16, 0, 2>,
+                                parity_kernel<2, 32, 0, 2>},
+                               {parity_kernel<2, 4, 32, 2>, parity_kernel<2, 8, 32, 2>, parity_kernel<2, 16, 32, 2>,
+                                parity_kernel<2, 32, 32, 2>}};
+    const int i0 = T0 == 4 ? 0 : T0 == 8 ? 1 : T0 == 16 ? 2 : 3;
+    kern = (n == 1 ? k1 : k2)[c1 > 0 ? 1 : 0][i0];
+    if (a.cnt[2] > 2) { cvd::set_error("parity_detect: duplicate terms"); return CVD_E_INVALID; }
+  }
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
   HIP_CHECK(hipGetLastError());
   return CVD_OK;
