@@ -59,9 +59,10 @@ def parse():
                          "(-1: auto = on for the table automaton, where it measured faster)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle port (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "detector_pmc.json"),
+    ap.add_argument("--pmc-traffic", default=None,
                     help="per-launch detector FETCH_SIZE summary of a rocprofv3 --pmc pass "
-                         "(profiles/collect.sh); used only when its config/batch/N match this run")
+                         "(profiles/collect.sh + summarize.py; default profiles/pmc_<detector>_<config>.json); "
+                         "used only when its config/batch/N match this run")
     return ap.parse_args()
 
 
@@ -191,6 +192,8 @@ def main():
     alg_bytes = B * 2 * ((N * n + 7) // 8)
     achieved = alg_bytes / (det_ms * 1e-3) / 1e9
     traffic, traffic_src, valu = None, None, None
+    if a.pmc_traffic is None:
+        a.pmc_traffic = os.path.join(ROOT, "profiles", f"pmc_{a.detector}_{a.config}.json")
     if a.pmc_traffic and os.path.exists(a.pmc_traffic):
         with open(a.pmc_traffic) as f:
             pmc = json.load(f)
@@ -217,7 +220,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u16x2 (metrics) + f64 (log-likelihood sums)",
         "data": "synthetic: Philox4x32-10 encoder inputs and BSC(p) flips (build spec), learned P̂1",
-        "config": {"workload": f"{a.config} pair {cc['gen1']} vs {cc['gen2']}, N={N}, p-sweep {p_grid}, "
+        "config": {"name": a.config, "detector": a.detector,
+                   "workload": f"{a.config} pair {cc['gen1']} vs {cc['gen2']}, N={N}, p-sweep {p_grid}, "
                                f"one p per step", "N": N, "p_grid": p_grid,
                    "trials_per_step_per_gpu": B, "model": info["kind"] and "sparse(learned)" or "dense",
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],

@@ -1,9 +1,9 @@
 """Turn a profiles/collect.sh output directory (gpurun_out/...) into the
 committed evidence: profiles/<name>/ (rocprofv3 kernel stats, trace and PMC
-CSVs trimmed to the detector and generator) and profiles/detector_pmc.json,
-which bench.py reads for roofline.traffic.
+CSVs trimmed to the detector and generator) and the per-launch PMC summary,
+which bench.py reads for roofline.traffic (profiles/pmc_<detector>_<config>.json).
 
-  python profiles/summarize.py gpurun_out/prof r01c
+  python profiles/summarize.py gpurun_out/prof r01d_m6
 """
 import csv
 import glob
@@ -16,7 +16,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def is_det(name):
-    return "detect" in name or "k1b" in name
+    return "detect" in name or "k1b" in name or "parity_kernel" in name
+
+
+def is_gen(name):
+    return "gen_" in name
 
 
 def main(src, name):
@@ -25,7 +29,7 @@ def main(src, name):
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))[0]
     shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
     trace = glob.glob(os.path.join(src, "trace", "*kernel_trace.csv"))[0]
-    rows = [r for r in csv.DictReader(open(trace)) if is_det(r["Kernel_Name"]) or "gen_kernel" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(trace)) if is_det(r["Kernel_Name"]) or is_gen(r["Kernel_Name"])]
     with open(os.path.join(dst, "kernel_trace.csv"), "w", newline="") as f:
         w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
         w.writeheader()
@@ -34,7 +38,7 @@ def main(src, name):
     json.dump(bench, open(os.path.join(dst, "bench_under_rocprof.json"), "w"), indent=1)
     agg, cnt = {}, {}
     for i, f in enumerate(sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")))):
-        keep = [r for r in csv.DictReader(open(f)) if is_det(r["Kernel_Name"]) or "gen_kernel" in r["Kernel_Name"]]
+        keep = [r for r in csv.DictReader(open(f)) if is_det(r["Kernel_Name"]) or is_gen(r["Kernel_Name"])]
         tag = os.path.basename(os.path.dirname(f))
         with open(os.path.join(dst, f"{tag}.csv"), "w", newline="") as g:
             w = csv.DictWriter(g, fieldnames=list(keep[0].keys()))
@@ -60,7 +64,7 @@ def main(src, name):
         "detector_fetch_bytes_per_launch": per.get("FETCH_SIZE", 0.0) * 1024 * 2,
         "correction": "x2 per MI355X_MICROARCH.md HBM section (FETCH_SIZE = half of a 16-B/lane streaming read); "
                       "the row-table traffic is 8-64 B random accesses, which that guide leaves uncalibrated",
-        "algorithmic_bytes_per_launch": 2 * B * ((N * 2 + 7) // 8),
+        "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
         "SQ_INSTS_VALU_per_launch": per.get("SQ_INSTS_VALU"),
         "VALU_insts_per_wave_step": per.get("SQ_INSTS_VALU", 0.0) / (waves * N),
         "SALU_insts_per_wave_step": per.get("SQ_INSTS_SALU", 0.0) / (waves * N),
@@ -76,11 +80,13 @@ def main(src, name):
         "wait_inst_any_frac_of_wave_cycles": per.get("SQ_WAIT_INST_ANY", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
         "active_valu_frac_of_wave_cycles": per.get("SQ_ACTIVE_INST_VALU", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
         "counters_per_launch": per,
-        "config": "m6",
+        "config": cfg.get("name", "m6"),
+        "detector": cfg.get("detector", "markov"),
         "batch": B,
         "N": N,
     }
-    json.dump(out, open(os.path.join(ROOT, "profiles", "detector_pmc.json"), "w"), indent=1)
+    fn = f"pmc_{out['detector']}_{out['config']}.json"
+    json.dump(out, open(os.path.join(ROOT, "profiles", fn), "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "counters_per_launch"}, indent=1))
 
 
