@@ -306,14 +306,56 @@ __device__ __forceinline__ void k1b_trace(uint8_t* tr, int64_t t, int64_t nseq, 
 constexpr int kK1bWavesPerSimd = 4;
 constexpr int kRenorm = 128;   // O <= 128: raw pair values stay < 256 (byte packing)
 
+// Register layouts of the pair vector.  Layout 0: register i holds
+// (D(2i), D(2i+1)).  Layout 1: register i holds (D(x), D(x+2)) with
+// x = 4(i >> 1) + (i & 1), so state s is in register 2(s >> 2) + (s & 1), half
+// (s >> 1) & 1.  Both keep states 8w..8w+3 / 8w+4..8w+7 in registers 4w, 4w+1 /
+// 4w+2, 4w+3, so one v_perm per half-word packs either into the device key.
+template <int L>
+__device__ constexpr int lay_reg(int s) { return L == 0 ? s >> 1 : (((s >> 2) << 1) | (s & 1)); }
+template <int L>
+__device__ constexpr int lay_half(int s) { return L == 0 ? (s & 1) : ((s >> 1) & 1); }
+
+// Branch-metric pair (e_j, 2 - e_j) of butterfly j for the lane's word:
+// out(j, 0) = bits 2j..2j+1 of XM, e = popcount(out ^ y), so out 3 and 2 give the
+// swaps of out 0 and 1 (W0 = (e0, 2 - e0), W1 = (e1, 2 - e1))
+template <uint64_t XM>
+__device__ __forceinline__ us2 bfly_w(int j, uint32_t W0, uint32_t W1) {
+  const int xj = (int)((XM >> (2 * j)) & 3u);
+  return xj == 0 ? as_us2(W0) : xj == 1 ? as_us2(W1) : xj == 2 ? __builtin_shufflevector(as_us2(W1), as_us2(W1), 1, 0)
+                                                         : __builtin_shufflevector(as_us2(W0), as_us2(W0), 1, 0);
+}
+// e(out) as the low half it takes in W0 / W1 (v_perm byte selectors)
+template <uint64_t XM>
+__device__ constexpr uint32_t e_sel(int j) {
+  const int xj = (int)((XM >> (2 * j)) & 3u);
+  // perm(W1, W0, .): selectors 0-3 = W0 bytes, 4-7 = W1 bytes.  e(out 0) = e0 = W0
+  // bytes 0-1, e(3) = 2 - e0 = W0 bytes 2-3, e(1) = e1 = W1 bytes 0-1, e(2) = 2 - e1
+  // = W1 bytes 2-3; the complement 2 - e(out) = e(out ^ 3) is selector ^ 0x0202
+  return xj == 0 ? 0x0100u : xj == 3 ? 0x0302u : xj == 1 ? 0x0504u : 0x0706u;
+}
+
 // The common step: D_t(y) for the lane's own word, in place in Dp (pair i is
 // dead once butterflies 2i, 2i + 1 and 2i - H, 2i + 1 - H have read it), and
 // the nibble keys of the raw metrics minus the running offset.
-template <int m, bool kSpec, uint64_t XM>
+//
+// kKind 0 (table-driven and general): layout 0 in and out; each butterfly is
+//   one packed add of the broadcast top input, one of the broadcast bottom input
+//   and one packed min (three VOP3P).
+// kKind 1 (specialised, even steps): layout 0 in, layout 1 out, no broadcast:
+//   butterflies j, j+1 (j even) share registers (D(j), D(j+1)) and
+//   (D(j+32), D(j+33)); adding (e_j, e_{j+1}) and (2-e_j, 2-e_{j+1}) as plain
+//   32-bit adds (two 16-bit lanes, no carry) and two packed mins give
+//   (D'(2j), D'(2j+2)) and (D'(2j+1), D'(2j+3)): four VOP2 + two VOP3P per two
+//   butterflies instead of six VOP3P.
+// kKind 2 (specialised, odd steps): layout 1 in (broadcast picks the half),
+//   layout 0 out.
+template <int m, bool kSpec, uint64_t XM, int kKind = 0>
 __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1 << m) / 8, 4>& cur, uint32_t rr,
                                         uint32_t (&Dp)[(1 << m) / 2], uint32_t (&kw)[(1 << m) / 8],
                                         uint32_t sel, uint32_t O8, uint32_t& zn) {
   constexpr int M = 1 << m, H = M / 2;
+  constexpr int LIN = kKind == 2 ? 1 : 0;
   uint32_t E[H];
   // specialised (kSpec, out(j, 0) = bits 2j..2j+1 of XM): the lane's pairs
   // (e, 2 - e) for out(j, 0) = 0 and 1; out 3 and 2 are their swaps (op_sel),
@@ -324,38 +366,62 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
     W0 = e0 | ((2u - e0) << 16);
     W1 = e1 | ((2u - e1) << 16);
   }
+  auto pack = [&](int w, uint32_t sel_pk) {
+    // word w = states 8w..8w+7 in nibble order bitrev3 (device key layout):
+    // bytes (s0, s2, s1, s3) and (s4, s6, s5, s7) by one v_perm each (metrics + O < 256)
+    const uint32_t x = __builtin_amdgcn_perm(E[4 * w + 1], E[4 * w], sel_pk);
+    const uint32_t y = __builtin_amdgcn_perm(E[4 * w + 3], E[4 * w + 2], sel_pk);
+    const uint32_t v = x + (y << 4) - O8;             // nibbles = raw metric - offset <= 14
+    zn |= (v - 0x11111111u) & ~v;
+    kw[w] = v;
+  };
+  if constexpr (kKind == 1) {
+    static_assert(kSpec, "no-broadcast step needs the specialised code");
 #pragma unroll
-  for (int j = 0; j < H; ++j) {
-    if (j == H / 2) {                   // filter positive: key + row loads under the second half
-      cur.fence(zn);                    // zn depends on every butterfly so far
-      cur.mid(a, rr);
+    for (int j = 0; j < H; j += 2) {
+      if (j == H / 2) {
+        cur.fence(zn);
+        cur.mid(a, rr);
+      }
+      const uint32_t ra = Dp[j >> 1], rb = Dp[(j >> 1) + H / 2];
+      // (e_j, e_{j+1}) and (2 - e_j, 2 - e_{j+1}) (compile-time selectors; the
+      // compiler shares equal ones across butterfly pairs)
+      const uint32_t ep = __builtin_amdgcn_perm(W1, W0, (e_sel<XM>(j + 1) << 16) | e_sel<XM>(j));
+      const uint32_t cp = __builtin_amdgcn_perm(W1, W0, ((e_sel<XM>(j + 1) ^ 0x0202u) << 16) | (e_sel<XM>(j) ^ 0x0202u));
+      E[j] = as_u32(__builtin_elementwise_min(as_us2(ra + ep), as_us2(rb + cp)));       // (D'(2j), D'(2j+2))
+      E[j + 1] = as_u32(__builtin_elementwise_min(as_us2(ra + cp), as_us2(rb + ep)));   // (D'(2j+1), D'(2j+3))
+      if ((j & 3) == 2) pack(j >> 2, 0x06040200u);
     }
-    const us2 pa = as_us2(Dp[j >> 1]), pb = as_us2(Dp[(j >> 1) + H / 2]);
-    const us2 da = (j & 1) ? __builtin_shufflevector(pa, pa, 1, 1) : __builtin_shufflevector(pa, pa, 0, 0);
-    const us2 db = (j & 1) ? __builtin_shufflevector(pb, pb, 1, 1) : __builtin_shufflevector(pb, pb, 0, 0);
-    us2 W;
-    if constexpr (kSpec) {
-      const int xj = (int)((XM >> (2 * j)) & 3u);
-      W = xj == 0 ? as_us2(W0) : xj == 1 ? as_us2(W1) : xj == 2 ? __builtin_shufflevector(as_us2(W1), as_us2(W1), 1, 0)
-                                                             : __builtin_shufflevector(as_us2(W0), as_us2(W0), 1, 0);
-    } else {
-      const uint32_t T = tb[j];
-      W = as_us2(__builtin_amdgcn_perm(T, T, sel));   // (e, 2 - e)
-    }
-    E[j] = as_u32(__builtin_elementwise_min(da + W, db + __builtin_shufflevector(W, W, 1, 0)));
-    if ((j & 3) == 3) {
-      // word w = states 8w..8w+7 in nibble order bitrev3 (device key layout):
-      // bytes (E0.lo, E1.lo, E0.hi, E1.hi) by one v_perm (metrics + O < 256)
-      const uint32_t x = __builtin_amdgcn_perm(E[j - 2], E[j - 3], 0x06020400u);
-      const uint32_t y = __builtin_amdgcn_perm(E[j], E[j - 1], 0x06020400u);
-      const uint32_t v = x + (y << 4) - O8;             // nibbles = raw metric - offset <= 14
-      zn |= (v - 0x11111111u) & ~v;
-      kw[j >> 2] = v;
+  } else {
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      if (j == H / 2) {                   // filter positive: key + row loads under the second half
+        cur.fence(zn);                    // zn depends on every butterfly so far
+        cur.mid(a, rr);
+      }
+      const us2 pa = as_us2(Dp[lay_reg<LIN>(j)]), pb = as_us2(Dp[lay_reg<LIN>(j + H)]);
+      const int h = lay_half<LIN>(j);
+      const us2 da = h ? __builtin_shufflevector(pa, pa, 1, 1) : __builtin_shufflevector(pa, pa, 0, 0);
+      const us2 db = h ? __builtin_shufflevector(pb, pb, 1, 1) : __builtin_shufflevector(pb, pb, 0, 0);
+      us2 W;
+      if constexpr (kSpec) {
+        W = bfly_w<XM>(j, W0, W1);
+      } else {
+        const uint32_t T = tb[j];
+        W = as_us2(__builtin_amdgcn_perm(T, T, sel));   // (e, 2 - e)
+      }
+      E[j] = as_u32(__builtin_elementwise_min(da + W, db + __builtin_shufflevector(W, W, 1, 0)));
+      if ((j & 3) == 3) pack(j >> 2, 0x06020400u);
     }
   }
 #pragma unroll
   for (int j = 0; j < H; ++j) Dp[j] = E[j];
 }
+
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
 
 template <int m, bool kSpec, uint64_t XM, bool kTrace>
 __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
@@ -397,14 +463,17 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     RowCursor<NW, R> cur;
     cur.start(a, cw & 3u);
 
-    // one step t (1-based) with received word rr and the next step's word rn
-    auto step = [&](uint32_t rr, uint32_t rn, int64_t t) {
+    // one step t (1-based) with received word rr and the next step's word rn;
+    // the specialised kernel alternates no-broadcast (layout 0 -> 1) and
+    // broadcast (1 -> 0) steps, so every even step leaves layout 0
+    auto step = [&](uint32_t rr, uint32_t rn, int64_t t, auto kind) {
+      constexpr int KIND = kSpec ? decltype(kind)::value : 0;
       const uint32_t sel = rr | ((rr ^ 3u) << 16) | 0x0C000C00u;
       cu32* tb = as_const(a.bmp);
       asm volatile("" : "+s"(tb));   // per step: the table is re-read (scalar cache), not held in SGPRs
       uint32_t kw[NW];
       uint32_t zn = 0u;
-      k1b_acs<m, kSpec, XM>(a, tb, cur, rr, Dp, kw, sel, O8, zn);
+      k1b_acs<m, kSpec, XM, KIND>(a, tb, cur, rr, Dp, kw, sel, O8, zn);
       // Eq. 5: step minimum 0 or 1
       const uint32_t mu = (zn & 0x88888888u) == 0u;
       const uint32_t mu8 = mu ? 0x11111111u : 0u;
@@ -449,8 +518,10 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     int g = 0;
     for (; t + 4 <= N; t += 4) {
       const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(nw, cw, 24);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) step(bits2(win, 2 * i), bits2(win, 2 * i + 2), t + i + 1);
+      step(bits2(win, 0), bits2(win, 2), t + 1, IntC<1>{});
+      step(bits2(win, 2), bits2(win, 4), t + 2, IntC<2>{});
+      step(bits2(win, 4), bits2(win, 6), t + 3, IntC<1>{});
+      step(bits2(win, 6), bits2(win, 8), t + 4, IntC<2>{});
       if (++g == 4) {
         g = 0;
         cw = nw;
@@ -468,7 +539,9 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     // last 1-3 steps (inside the current group, so no renormalisation is due)
     if (t < N) {
       const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(nw, cw, 24);
-      for (int i = 0; t < N; ++i, ++t) step(bits2(win, 2 * i), bits2(win, 2 * i + 2), t + 1);
+      step(bits2(win, 0), bits2(win, 2), t + 1, IntC<1>{});
+      if (t + 1 < N) step(bits2(win, 2), bits2(win, 4), t + 2, IntC<2>{});
+      if (t + 2 < N) step(bits2(win, 4), bits2(win, 6), t + 3, IntC<1>{});
     }
     if (a.sums) {
       const int64_t qe = qwave + lane_id();
