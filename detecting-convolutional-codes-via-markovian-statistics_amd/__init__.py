@@ -16,3 +16,7 @@ from .parity import (  # noqa: F401
     template_of, default_template, parity_detect, parity_satisfaction_fraction, parity_detector,
     parity_experiment,
 )
+from .exponent import (  # noqa: F401
+    TransitionTensor, learn_transition_tensor, chernoff_rhos, compute_error_exponent, spectral_radius,
+    fit_error_exponent, EXPONENT_TAG,
+)

@@ -82,6 +82,16 @@ EXPORTS = {
     "cvd_parity_detect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
                                          ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "cvd_count_transitions": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "cvd_chernoff_build": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_double, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "cvd_chernoff_build_dense": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    "cvd_spectral_radius": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, ctypes.c_int32,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _lib = None

@@ -89,6 +89,8 @@ int upload_model(cvd_model& M, int device);
 // CVD_KERNEL_* that launch_detect_explicit(kExplicitBest) picks for this model
 int explicit_kernel_of(const cvd_model& M);
 // hipRTC-compiled code-specialised butterfly kernel (cvd_rtc.cpp); 0 = ok
+// CVD_OK if the model is uploaded to the current device
+int check_device(const cvd_model& M);
 int rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);

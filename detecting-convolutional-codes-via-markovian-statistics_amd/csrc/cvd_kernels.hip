@@ -821,14 +821,6 @@ ExpKernel pick_explicit(int m, int k, int n) {
   return nullptr;
 }
 
-int check_device(const cvd_model& M) {
-  if (M.device < 0) { set_error("model not uploaded (cvd_model_upload)"); return CVD_E_STATE; }
-  int cur = -1;
-  HIP_CHECK(hipGetDevice(&cur));
-  if (cur != M.device) { set_error("current device differs from the model's device"); return CVD_E_INVALID; }
-  return CVD_OK;
-}
-
 template <typename T>
 int dev_copy(T*& d, const std::vector<T>& h) {
   if (h.empty()) return CVD_OK;
@@ -840,6 +832,14 @@ int dev_copy(T*& d, const std::vector<T>& h) {
 }  // namespace
 
 // ───────────────────────────── launchers ─────────────────────────────────────
+
+int cvd::check_device(const cvd_model& M) {
+  if (M.device < 0) { set_error("model not uploaded (cvd_model_upload)"); return CVD_E_STATE; }
+  int cur = -1;
+  HIP_CHECK(hipGetDevice(&cur));
+  if (cur != M.device) { set_error("current device differs from the model's device"); return CVD_E_INVALID; }
+  return CVD_OK;
+}
 
 int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, uint64_t thr,
                          int64_t N, int random_input, int64_t seq_base, int64_t seq_stride,

@@ -16,6 +16,10 @@
  *   (none: the reference is single-process)                                        counts reduced by the caller over RCCL
  *   comp_parity.py:90-128     parity_satisfaction_fraction / parity_detector       cvd_parity_detect
  *                             (parity-template baseline)
+ *   alpha_exponent.py:83-156  learn_transition_tensor (joint counts)              cvd_count_transitions
+ *   alpha_exponent.py:159-188 compute_error_exponent: M(u) for a u grid           cvd_chernoff_build(_dense)
+ *   alpha_exponent.py:69-76   spectral_radius (Perron root of M(u) >= 0)           cvd_spectral_radius
+ *                             (error-exponent engine)
  *
  * Conventions:
  *   - every function returns 0 on success, a negative CVD_E* code on error;
@@ -166,6 +170,32 @@ int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc
 int cvd_parity_detect(const uint32_t* d_r, int32_t n, int64_t N, int64_t nseq, int64_t n_h1,
                       const int32_t* terms, int32_t n_terms, double gamma, int32_t* d_sat,
                       int64_t* d_counts, void* stream);
+
+/* ---- error-exponent engine (alpha_exponent.py, Eq. 7) ---------------------
+ * Joint counts of (metric state i, received word r) along received streams
+ * (pitch = nseq) for steps t >= burn_in, on a dense (enumerated) model with
+ * S < 4096: d_cnt[i*2^n + r] += count (uint64, accumulated, not cleared).
+ * The chain's next state is the model's automaton (alpha_exponent.py:136-149). */
+int cvd_count_transitions(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
+                          int64_t burn_in, uint64_t* d_cnt, void* stream);
+/* M(u) = sum_r P1(i->j,r)^u P2(i->j,r)^(1-u) for u = d_u[0..U) from joint counts
+ * cnt1/cnt2 [K*R] (f64) of tensors P = (C + laplace) / rowsum over (j, r)
+ * (alpha_exponent.py:152-154), C[i,j,r] = cnt[i,r] iff j = next(i,r): written as
+ * d_a[U*K] (rank-one part, M += a 1^T) and d_vals[U*K*R] (entry (i, next(i,r))). */
+int cvd_chernoff_build(int32_t K, int32_t R, const double* d_cnt1, const double* d_cnt2, double laplace,
+                       const double* d_u, int32_t U, double* d_a, double* d_vals, void* stream);
+/* Dense M(u)[i][j] (d_vals[U*K*K]) from arbitrary P1, P2 [K*K*R] (alpha_exponent.py:170-180). */
+int cvd_chernoff_build_dense(int32_t K, int32_t R, const double* d_P1, const double* d_P2,
+                             const double* d_u, int32_t U, double* d_vals, void* stream);
+/* Perron root of each of U nonnegative K x K matrices M = a 1^T + ELL(vals, cols)
+ * (E entries per row; d_cols NULL: dense rows, E = K; d_a NULL: no rank-one part)
+ * by power iteration with Collatz-Wielandt bounds: d_rho[3u..3u+2] = (estimate,
+ * lower, upper bound) once (upper - lower) <= tol * upper (irreducible M), else
+ * once the power-iteration norm ratio is stable to tol/100 (the estimate), or
+ * after max_iter iterations (d_iters[u]).  K <= 10000. */
+int cvd_spectral_radius(int32_t K, int32_t E, const double* d_a, const double* d_vals,
+                        const int32_t* d_cols, int32_t U, double tol, int32_t max_iter, double* d_rho,
+                        int32_t* d_iters, void* stream);
 
 #ifdef __cplusplus
 }
