@@ -41,6 +41,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, one GPU per rank); gloo only to rehearse the multi-rank path")
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="m6", choices=["m6", "m2", "r23_m4"])
@@ -72,11 +74,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dist_backend == "gloo" and os.environ.get("CVD_BENCH_ONE_DEVICE") == "1":
+        local = 0   # rehearsal of the multi-rank path on a one-GPU box (RCCL needs one GPU per rank)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     cc = pkg.CONFIG_CODES[a.config]
     k, n, m = cc["k"], cc["n"], cc["m"]
