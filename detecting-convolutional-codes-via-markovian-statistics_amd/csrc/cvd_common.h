@@ -34,7 +34,14 @@ CVD_HD U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0
     const uint64_t p0 = (uint64_t)kPhiloxM0 * c0, p1 = (uint64_t)kPhiloxM1 * c2;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one v_bitop3_b32 (xor3, truth table 0x96) per output word; LLVM otherwise emits two v_xor_b32
+    uint32_t n0, n2;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c1), "s"(k0));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c3), "s"(k1));
+#else
     const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+#endif
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += kPhiloxW0; k1 += kPhiloxW1;
   }

@@ -268,19 +268,28 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
           for (int e = 0; e < GW; ++e) nm[e] = ~0u;
         } else {
           const uint32_t b0 = (uint32_t)(wg * NBITS / 4);
+          // blocks in groups of kPG: the group's Philox chains are independent
+          // (interleaved by the scheduler), then its flips shift in, highest first
+          constexpr int kPG = NB % 4 == 0 ? 4 : NB % 3 == 0 ? 3 : 1;
 #pragma unroll
-          for (int bb = NB - 1; bb >= 0; --bb) {
+          for (int g0 = NB - kPG; g0 >= 0; g0 -= kPG) {
             // launder the (uniform) key so its 10-round schedule is recomputed
-            // by scalar adds per call instead of being hoisted into SGPRs
+            // by scalar adds per group instead of being hoisted into SGPRs
             uint32_t k0 = a.k0, k1 = a.k1;
             asm volatile("" : "+s"(k0), "+s"(k1));
-            const U4 x = philox(b0 + (uint32_t)bb, slo, nhi, a.tag, k0, k1);
-            const uint32_t xv[4] = {x.x, x.y, x.z, x.w};
+            uint32_t xv[kPG][4];
 #pragma unroll
-            for (int e = 3; e >= 0; --e) {
-              const int ew = (4 * bb + e) / NBITS;
-              nm[ew] = shift_in_flip(nm[ew], xv[e], a.thr_lo);
+            for (int gb = 0; gb < kPG; ++gb) {
+              const U4 x = philox(b0 + (uint32_t)(g0 + gb), slo, nhi, a.tag, k0, k1);
+              xv[gb][0] = x.x; xv[gb][1] = x.y; xv[gb][2] = x.z; xv[gb][3] = x.w;
             }
+#pragma unroll
+            for (int gb = kPG - 1; gb >= 0; --gb)
+#pragma unroll
+              for (int e = 3; e >= 0; --e) {
+                const int ew = (4 * (g0 + gb) + e) / NBITS;
+                nm[ew] = shift_in_flip(nm[ew], xv[gb][e], a.thr_lo);
+              }
           }
         }
       }
