@@ -303,7 +303,16 @@ __device__ __forceinline__ void k1b_trace(uint8_t* tr, int64_t t, int64_t nseq, 
 // subtraction per word (exact modulo 2^32).  The step minimum is 0 or 1
 // (n = 2; D_{t-1} has a 0 state and one of its branches has metric <= 1), so it
 // is read off a zero-nibble test.
-constexpr int kK1bWavesPerSimd = 4;
+// Tuning knobs of the run-time compiled kernel (CVD_JIT_DEFINES="-D...",
+// cvd_rtc.cpp): occupancy target, and the quarter of the step at which a
+// filter-positive lookup issues its key and row loads.
+#ifndef CVD_K1B_WAVES
+#define CVD_K1B_WAVES 4
+#endif
+#ifndef CVD_K1B_MID
+#define CVD_K1B_MID 2
+#endif
+constexpr int kK1bWavesPerSimd = CVD_K1B_WAVES;
 constexpr int kRenorm = 128;   // O <= 128: raw pair values stay < 256 (byte packing)
 
 // Register layouts of the pair vector.  Layout 0: register i holds
@@ -356,6 +365,7 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
                                         uint32_t sel, uint32_t O8, uint32_t& zn) {
   constexpr int M = 1 << m, H = M / 2;
   constexpr int LIN = kKind == 2 ? 1 : 0;
+  constexpr int kMid = ((H * CVD_K1B_MID) / 4) & ~1;   // even: both loops reach it
   uint32_t E[H];
   // specialised (kSpec, out(j, 0) = bits 2j..2j+1 of XM): the lane's pairs
   // (e, 2 - e) for out(j, 0) = 0 and 1; out 3 and 2 are their swaps (op_sel),
@@ -379,7 +389,7 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
     static_assert(kSpec, "no-broadcast step needs the specialised code");
 #pragma unroll
     for (int j = 0; j < H; j += 2) {
-      if (j == H / 2) {
+      if (j == kMid) {
         cur.fence(zn);
         cur.mid(a, rr);
       }
@@ -395,7 +405,7 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
   } else {
 #pragma unroll
     for (int j = 0; j < H; ++j) {
-      if (j == H / 2) {                   // filter positive: key + row loads under the second half
+      if (j == kMid) {                   // filter positive: key + row loads under the second half
         cur.fence(zn);                    // zn depends on every butterfly so far
         cur.mid(a, rr);
       }

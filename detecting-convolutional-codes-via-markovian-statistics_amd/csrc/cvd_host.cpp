@@ -676,7 +676,7 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
     // ── sparse model: rows = states visited by the learning chain ──
     // The reference's semantics need the full BFS index (Pd_plotter.py:136-139,
     // 166-167), infeasible here (m = 6: > 2e8 states).  Declared policy
-    // (deviation D3): the state set is the chain's visited states
+    // (deviation D4): the state set is the chain's visited states
     // D_0..D_L in first-visit order, S = their number, unvisited rows are the
     // all-zero-count row λ / (S λ).
     Mo->kind = 1;

@@ -43,7 +43,7 @@ extern char** environ;
 namespace {
 
 std::mutex g_mu;
-std::map<std::tuple<int, int, uint64_t>, hipFunction_t> g_cache;
+std::map<std::tuple<int, int, uint64_t, std::string>, hipFunction_t> g_cache;
 
 std::string entry_source(int m, uint64_t xm) {
   char entry[256];
@@ -85,6 +85,12 @@ bool compile_clang(const std::string& src, const std::string& arch, std::vector<
   const std::string arch_opt = "--offload-arch=" + arch;
   std::vector<std::string> args = {clang, "-x", "hip", arch_opt, "--offload-device-only", "--no-gpu-bundle-output",
                                    "-O3", "-std=c++17", "-ffp-contract=off", "-c", in, "-o", out};
+  if (const char* d = std::getenv("CVD_JIT_DEFINES")) {   // tuning experiments: extra -D options only
+    std::istringstream ds(d);
+    std::string t;
+    while (ds >> t)
+      if (t.rfind("-D", 0) == 0) args.insert(args.end() - 4, t);
+  }
   std::vector<char*> argv;
   for (auto& s : args) argv.push_back(&s[0]);
   argv.push_back(nullptr);
@@ -147,7 +153,8 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out) {
   if (const char* e = std::getenv("CVD_NO_JIT"))
     if (e[0] && e[0] != '0') { set_error("JIT: disabled by CVD_NO_JIT"); return -1; }
   std::lock_guard<std::mutex> lock(g_mu);
-  const auto key = std::make_tuple(device, m, xm);
+  const char* defs = std::getenv("CVD_JIT_DEFINES");
+  const auto key = std::make_tuple(device, m, xm, std::string(defs ? defs : ""));
   auto it = g_cache.find(key);
   if (it != g_cache.end()) {
     *fn_out = (void*)it->second;

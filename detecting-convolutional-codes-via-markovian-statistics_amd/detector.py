@@ -177,9 +177,21 @@ class Detector:
                                         ctypes.c_void_p(D.data_ptr()), _stream_ptr(stream)))
         return D
 
-    def default_batch(self, N, trial_count, budget_bytes=4 << 30):
+    # one residency round of the butterfly kernel: 4 waves/SIMD x 1024 SIMDs x 64
+    # lanes = 262,144 sequences = 131,072 trials (H1 + H2)
+    FULL_ROUND_TRIALS = 131_072
+
+    def default_batch(self, N, trial_count, budget_bytes=None):
+        """Trials per launch: as many as a third of the free HBM (at most 96 GiB)
+        holds, rounded down to whole residency rounds when that is >= one round."""
         per_trial = 2 * self.words_per_seq(N) * 4
-        return int(max(1, min(trial_count, max(1024, budget_bytes // max(per_trial, 1)))))
+        if budget_bytes is None:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            budget_bytes = min(free // 3, 96 << 30)
+        b = max(1024, budget_bytes // max(per_trial, 1))
+        if b >= self.FULL_ROUND_TRIALS:
+            b -= b % self.FULL_ROUND_TRIALS
+        return int(max(1, min(trial_count, b)))
 
     def run_trials(self, model, gen1, gen2, N, p, seed, trial_begin, trial_end, batch=None,
                    path=_lib.PATH_AUTO, return_sums=False, counts=None, stream=None):

@@ -19,7 +19,7 @@
  * Row sums use the closed form R_i + S*laplace, equal to numpy's pairwise sum
  * for integral laplace (the only case the C oracle is used for).
  * Non-enumerable codes (m = 6) use the build's declared sparse policy
- * (DESIGN.md deviation D3): states = those visited by the learning chain.
+ * (DESIGN.md deviation D4): states = those visited by the learning chain.
  * Pinned against the Python restatement (tests/test_c_oracle.py), which is
  * pinned bit-exactly to the reference's golden vectors.
  */
