@@ -21,7 +21,7 @@ def test_experiment_csv(cli, pkg, tmp_path):
     cc = pkg.CONFIG_CODES["m2"]
     want = pkg.run_experiment(1, 2, 2, cc["gen1"], cc["gen2"], 300, [0.05, 0.2], None, 200, 1.0, 12345,
                               N_list=[60, 200])
-    assert pd.read_csv(out).to_dict(orient="records") == want.to_dict(orient="records")
+    assert pd.read_csv(out, float_precision="round_trip").to_dict(orient="records") == want.to_dict(orient="records")
 
 
 def test_parity_csv(cli, pkg, tmp_path):
@@ -30,7 +30,7 @@ def test_parity_csv(cli, pkg, tmp_path):
               "--gamma", "0.7", "--out", str(out)])
     cc = pkg.CONFIG_CODES["m2"]
     want = pkg.parity_experiment(1, 2, 2, cc["gen1"], cc["gen2"], 200, [0.02, 0.1], 0.7, 12345, N_list=[80])
-    assert pd.read_csv(out).to_dict(orient="records") == want.to_dict(orient="records")
+    assert pd.read_csv(out, float_precision="round_trip").to_dict(orient="records") == want.to_dict(orient="records")
 
 
 def test_exponent_csv(cli, pkg, tmp_path):
@@ -41,5 +41,5 @@ def test_exponent_csv(cli, pkg, tmp_path):
     P1 = pkg.learn_transition_tensor(c["gen1"], c["gen1"], 2, 0.05, 20000, 500, 1.0, 12345)[0]
     P2 = pkg.learn_transition_tensor(c["gen2"], c["gen1"], 2, 0.05, 20000, 500, 1.0, 12346)[0]
     I_err, u = pkg.compute_error_exponent(P1, P2, u_grid=41)
-    row = pd.read_csv(out).to_dict(orient="records")[0]
+    row = pd.read_csv(out, float_precision="round_trip").to_dict(orient="records")[0]
     assert (row["I_err"], row["u_star"], row["states"]) == (I_err, u, 31)
