@@ -9,7 +9,7 @@ by the defines).  One batch of streams per p is generated once; then
 rounds x variants detector launches are timed with HIP events on the launch
 stream, and every variant's per-trial sums must equal the first variant's.
 
-usage: python profiles/ab_k1b.py --variants "" "-DCVD_K1B_WAVES=5" --p 0.01 0.1
+usage: python profiles/ab_k1b.py --variant= --variant=-DCVD_K1B_WAVES=5 --p 0.01 0.1
 prints one JSON line per p: per-variant launch times (ms), medians and mins.
 """
 import argparse
@@ -27,7 +27,8 @@ from __graft_entry__ import load_package  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", nargs="+", default=[""])
+    ap.add_argument("--variant", action="append", dest="variants", default=None,
+                    help="CVD_JIT_DEFINES of one variant, as --variant=-DX=1 (empty: the default kernel)")
     ap.add_argument("--p", type=float, nargs="+", default=[0.01, 0.1])
     ap.add_argument("--trials", type=int, default=655_360,
                     help="trials per launch (655,360 = 5 rounds at 4 waves/SIMD, 4 rounds at 5)")
@@ -36,6 +37,7 @@ def main():
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--out", default=None, help="append the JSON lines to this file")
     a = ap.parse_args()
+    a.variants = a.variants or [""]
     pkg = load_package()
     cc = pkg.CONFIG_CODES["m6"]
     det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
