@@ -10,10 +10,13 @@
   ... exponent ...
       alpha_exponent.py -- learned transition tensors of G1 and G2 streams on
       G1's metric automaton, Eq. 7 per p, writes <save-dir>/error_exponent.csv
+  ... compare --hybrid H.csv --baseline B.csv [--outdir plots]
+      plots_compare.py:70-148 -- P_err = 1 - Pc of both detectors against p
+      (per N) and against N (per p), one PNG each (host only, matplotlib)
 
 Codes: the BASELINE configurations (m2, m6, r23_m4) or the demo presets
-(example:1, example:2, demo_script.py:35-52).  Every subcommand runs on the
-GPU through libcvd.so.  Under torchrun (one process per GPU) the trials are
+(example:1, example:2, demo_script.py:35-52).  Every subcommand but compare
+runs on the GPU through libcvd.so.  Under torchrun (one process per GPU) the trials are
 sharded over the ranks, the counts reduced with one all_reduce, and rank 0
 writes the CSV.
 """
@@ -81,6 +84,11 @@ def parser():
     x.add_argument("--laplace", type=float, default=1.0)
     x.add_argument("--chains", type=int, default=1, help="independent chains (1: the reference's one chain)")
     x.add_argument("--u-grid", type=int, default=401)
+
+    c = sub.add_parser("compare", help="P_err figures of both detectors (plots_compare.py)")
+    c.add_argument("--hybrid", required=True, help="CSV of the experiment subcommand")
+    c.add_argument("--baseline", required=True, help="CSV of the parity subcommand")
+    c.add_argument("--outdir", default="plots")
     return ap
 
 
@@ -127,6 +135,11 @@ def cmd_exponent(a):
 
 def main(argv=None):
     a = parser().parse_args(argv)
+    if a.cmd == "compare":
+        from .compare import compare_figures
+        for path in compare_figures(a.hybrid, a.baseline, a.outdir):
+            print("Saved", path)
+        return 0
     dist = _init_dist()
     run = {"experiment": cmd_experiment, "parity": cmd_parity, "exponent": cmd_exponent}[a.cmd]
     df, name, title = run(a)

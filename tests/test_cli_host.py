@@ -1,6 +1,7 @@
 """Command-line front end (package __main__): argument parsing and code
 selection, no GPU (the subcommands themselves: tests/test_gpu_cli.py)."""
 import importlib
+import os
 
 import pytest
 
@@ -34,3 +35,26 @@ def test_code_names(cli, pkg):
             cli.code_of(bad)
     with pytest.raises(SystemExit):
         cli.parser().parse_args(["bogus"])
+
+
+def test_compare_figures(cli, pkg, tmp_path):
+    """compare: P_err = clip(1 - Pc) curves per N and per p (plots_compare.py:35-134)."""
+    import pandas as pd
+    from importlib import import_module
+    cmp = import_module(pkg.__name__ + ".compare")
+    h = pd.DataFrame({"N": [100, 100, 500, 500], "p": [0.01, 0.1, 0.01, 0.1],
+                      "Pd": [1.0, 0.8, 1.0, 0.9], "Pc": [1.0, 0.85, 1.0, 0.95]})
+    b = pd.DataFrame({"N": [100, 100], "p": [0.01, 0.1], "Pd": [0.7, 0.55]})   # Pd only: used as Pc
+    cv = cmp.curves(h, b)
+    assert set(cv) == {("N", 100), ("N", 500), ("p", 0.01), ("p", 0.1)}
+    x, y = cv[("N", 100)]["hybrid"]
+    assert list(x) == [0.01, 0.1] and list(y) == [0.0, 1.0 - 0.85]
+    x, y = cv[("p", 0.1)]["baseline"]
+    assert list(x) == [100] and list(y) == [1.0 - 0.55]
+    assert len(cv[("N", 500)]["baseline"][0]) == 0
+    hp, bp = tmp_path / "h.csv", tmp_path / "b.csv"
+    h.to_csv(hp, index=False)
+    b.to_csv(bp, index=False)
+    assert cli.main(["compare", "--hybrid", str(hp), "--baseline", str(bp), "--outdir", str(tmp_path / "plots")]) == 0
+    assert sorted(os.listdir(tmp_path / "plots")) == ["Perr_vs_N_p0.01.png", "Perr_vs_N_p0.1.png",
+                                                      "Perr_vs_p_N100.png", "Perr_vs_p_N500.png"]
