@@ -326,3 +326,23 @@ def _three_explicit_paths_agree(pkg, k, n, m, t1, t2, N, p, learn_len=None):
     if m < 6 and model.info()["kind"] == 0:
         c = det.run_trials(model, t1, t2, N, p, 77, 0, 300, path=pkg.PATH_TABLE, return_sums=True)
         assert np.array_equal(a["sums"], c["sums"])
+
+
+@pytest.mark.parametrize("p", [0.01, 0.1])
+def test_m6_headline_config_sums_vs_c_oracle(pkg, dev, p):
+    """The bench workload itself (m = 6 pair, N = 1e5, the default 10^6-step
+    sparse model): per-trial fp64 sums of the code-specialised kernel equal the C
+    oracle's bit for bit, for the first trials and for trial ids past 10^6."""
+    from oracle import c_oracle as C
+    cc = pkg.CONFIG_CODES["m6"]
+    N, seed = 100_000, 12345
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    model = det.model(p, None, 200, 1.0, seed)
+    assert model.info()["kind"] == 1 and "spec" in pkg.KERNEL_NAMES[model.info()["explicit_kernel"]]
+    c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
+    cm = C.Model(c1, p, None, 200, 1.0, seed)
+    for t0, t1 in ((0, 12), (1_000_003, 1_000_011)):
+        got = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, t0, t1, return_sums=True)
+        cnt, want = cm.run_trials(c1, c2, N, p, seed, t0, t1, sums=True)
+        assert np.array_equal(got["sums"], want)
+        assert tuple(got["counts"].cpu().tolist()) == tuple(int(x) for x in cnt)
