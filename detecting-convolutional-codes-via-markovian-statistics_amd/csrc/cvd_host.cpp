@@ -320,28 +320,30 @@ struct VirtualRow {
   double lam;
   const std::vector<std::pair<int64_t, double>>* sp;
   std::unordered_map<int64_t, double>* memo;
-  double at(int64_t j) const {
-    auto it = std::lower_bound(sp->begin(), sp->end(), std::make_pair(j, -1e308));
-    if (it != sp->end() && it->first == j) return it->second;
-    return lam;
-  }
   bool has_special(int64_t off, int64_t n) const {
     auto it = std::lower_bound(sp->begin(), sp->end(), std::make_pair(off, -1e308));
     return it != sp->end() && it->first < off + n;
   }
   double leaf(int64_t off, int64_t n) const {
+    // the block's values materialised once (lam, with the few specials patched in),
+    // then numpy's leaf arithmetic on them, in numpy's order
+    double v[128];
+    for (int64_t i = 0; i < n; ++i) v[i] = lam;
+    for (auto it = std::lower_bound(sp->begin(), sp->end(), std::make_pair(off, -1e308));
+         it != sp->end() && it->first < off + n; ++it)
+      v[it->first - off] = it->second;
     if (n < 8) {
       double res = 0.;
-      for (int64_t i = 0; i < n; ++i) res += at(off + i);
+      for (int64_t i = 0; i < n; ++i) res += v[i];
       return res;
     }
     double r[8];
-    for (int e = 0; e < 8; ++e) r[e] = at(off + e);
+    for (int e = 0; e < 8; ++e) r[e] = v[e];
     int64_t i = 8;
     for (; i < n - (n % 8); i += 8)
-      for (int e = 0; e < 8; ++e) r[e] += at(off + i + e);
+      for (int e = 0; e < 8; ++e) r[e] += v[i + e];
     double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res += at(off + i);
+    for (; i < n; ++i) res += v[i];
     return res;
   }
   double pw(int64_t off, int64_t n) const {
