@@ -311,7 +311,10 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
             uint32_t o = 0u;
 #pragma unroll
             for (int r = 0; r < k; ++r) {
-              const uint32_t tm = a.taps[j][r];
+              // the tap mask is re-read per word: hoisted out of the chunk loop, its
+              // per-shift branch conditions fill the SGPRs (spills through v_writelane)
+              uint32_t tm = a.taps[j][r];
+              asm volatile("" : "+s"(tm));
 #pragma unroll
               for (int sh = 0; sh <= kMaxM; ++sh)
                 if ((tm >> sh) & 1u) o ^= Wr[r] >> sh;
