@@ -20,6 +20,11 @@
 //                             iteration on the positive matrix with Collatz-
 //                             Wielandt bounds  min_i (Mx)_i/x_i <= rho <= max_i (Mx)_i/x_i
 //                             until they agree to `tol` (Perron-Frobenius: M > 0)
+//   rho_*_kernel              the same iteration for K above the LDS limit (the
+//                             m = 4 rate-1/2 automata, K = 150,743): vectors in
+//                             HBM, every u at once, one launch per phase
+//   count_transitions_global_kernel  the joint counts for S >= 4096 (records read
+//                             from L2, global atomics)
 //
 // These are the math of alpha_exponent.py; the reference's np.linalg.eigvals
 // (alpha_exponent.py:69-76) is replaced by the Perron root, which equals the
@@ -28,7 +33,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "../../include/cvd.h"
 #include "cvd_internal.h"
@@ -93,6 +100,29 @@ __global__ __launch_bounds__(kCountBlock) void count_transitions_kernel(CountArg
     __syncthreads();
     for (int i = threadIdx.x; i < SR; i += kCountBlock)
       if (s_hist[i]) atomicAdd(&a.cnt[i], (unsigned long long)s_hist[i]);
+  }
+}
+
+// S >= 4096: the 32-bit records stay in global memory (L2-resident: 2.4 MB at
+// S = 150,743, n = 2) and every count is a global atomic
+template <int n>
+__global__ __launch_bounds__(256) void count_transitions_global_kernel(CountArgs a) {
+  constexpr int R = 1 << n, SPW = 32 / n;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= a.nseq) return;
+  const int64_t nwords = (a.N + SPW - 1) / SPW;
+  uint32_t st = 0;
+  for (int64_t w = 0; w < nwords; ++w) {
+    uint32_t word = a.r[((w >> 2) * a.nseq + q) * 4 + (w & 3)];
+    const int64_t t0 = w * SPW;
+    const int ns = (int)min((int64_t)SPW, a.N - t0);
+    for (int i = 0; i < ns; ++i) {
+      const uint32_t rr = word & (uint32_t)(R - 1);
+      word >>= n;
+      const uint64_t idx = (uint64_t)st * R + rr;
+      if (t0 + i >= a.burn) atomicAdd(&a.cnt[idx], 1ull);
+      st = a.rec[idx] >> 4;
+    }
   }
 }
 
@@ -247,6 +277,163 @@ __global__ __launch_bounds__(kRhoBlock) void spectral_radius_kernel(RhoArgs p) {
   }
 }
 
+// ─────────────── spectral radius for K above the LDS limit ───────────────
+// The iteration of spectral_radius_kernel with x, y in HBM for all u at once:
+// rho_matvec (y = M x, per-block Collatz-Wielandt min / max and max y), rho_step
+// (per u: the bounds, the stopping tests, the next scale), rho_scale (x = y /
+// ymax, per-block sums), rho_sum (per u: 1^T x for the rank-one part).  State
+// per u in st[8]: 0 sx, 1 est, 2 prev, 3 lo, 4 hi, 5 ymax, 6 done (1 bounds met,
+// 2 stopped on the norm ratio), 7 iterations.
+constexpr int kGBlock = 256;
+
+struct GRhoArgs {
+  int32_t K, E, nb;
+  const double* a;
+  const double* vals;
+  const int32_t* cols;
+  double* x;
+  double* y;
+  double* part;   // [U][nb][3]
+  double* st;     // [U][8]
+  double tol;
+};
+
+__global__ __launch_bounds__(kGBlock) void rho_matvec_kernel(GRhoArgs g) {
+  __shared__ double s_red[kGBlock / 64];
+  const int u = blockIdx.y;
+  const double* st = g.st + 8 * u;
+  if (st[6] != 0.0) return;   // uniform per block
+  const int i = blockIdx.x * kGBlock + threadIdx.x;
+  double rmin = 1e308, rmax = 0.0, ym = 0.0;
+  if (i < g.K) {
+    const int64_t ui = (int64_t)u * g.K + i;
+    const double* xu = g.x + (int64_t)u * g.K;
+    double s = g.a ? g.a[ui] * st[0] : 0.0;
+    const double* row = g.vals + ui * g.E;
+    const int32_t* cr = g.cols + (int64_t)i * g.E;
+    for (int e = 0; e < g.E; ++e) s += row[e] * xu[cr[e]];
+    g.y[ui] = s;
+    rmin = rmax = s / xu[i];
+    ym = s;
+  }
+  rmin = block_reduce(rmin, s_red, 1);
+  rmax = block_reduce(rmax, s_red, 2);
+  ym = block_reduce(ym, s_red, 2);
+  if (threadIdx.x == 0) {
+    double* pp = g.part + ((int64_t)u * g.nb + blockIdx.x) * 3;
+    pp[0] = rmin; pp[1] = rmax; pp[2] = ym;
+  }
+}
+
+__global__ __launch_bounds__(kGBlock) void rho_step_kernel(GRhoArgs g) {
+  __shared__ double s_red[kGBlock / 64];
+  const int u = blockIdx.x;
+  double* st = g.st + 8 * u;
+  if (st[6] != 0.0) return;
+  double lo = 1e308, hi = 0.0, ym = 0.0;
+  for (int b = threadIdx.x; b < g.nb; b += kGBlock) {
+    const double* pp = g.part + ((int64_t)u * g.nb + b) * 3;
+    lo = fmin(lo, pp[0]); hi = fmax(hi, pp[1]); ym = fmax(ym, pp[2]);
+  }
+  lo = block_reduce(lo, s_red, 1);
+  hi = block_reduce(hi, s_red, 2);
+  ym = block_reduce(ym, s_red, 2);
+  if (threadIdx.x == 0) {
+    st[3] = lo; st[4] = hi; st[1] = ym; st[5] = ym;
+    st[7] += 1.0;
+    if (hi - lo <= g.tol * hi) st[6] = 1.0;
+    else if (!(ym > 0.0) || fabs(ym - st[2]) <= 0.01 * g.tol * ym) st[6] = 2.0;
+    else st[2] = ym;
+  }
+}
+
+__global__ __launch_bounds__(kGBlock) void rho_scale_kernel(GRhoArgs g) {
+  __shared__ double s_red[kGBlock / 64];
+  const int u = blockIdx.y;
+  const double* st = g.st + 8 * u;
+  if (st[6] != 0.0) return;
+  const int i = blockIdx.x * kGBlock + threadIdx.x;
+  double v = 0.0;
+  if (i < g.K) {
+    const int64_t ui = (int64_t)u * g.K + i;
+    v = g.y[ui] / st[5];
+    g.x[ui] = v;
+  }
+  v = block_reduce(v, s_red, 0);
+  if (threadIdx.x == 0) g.part[((int64_t)u * g.nb + blockIdx.x) * 3] = v;
+}
+
+__global__ void rho_sum_kernel(GRhoArgs g, int32_t U) {   // one thread per u, blocks in order
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U || g.st[8 * u + 6] != 0.0) return;
+  double s = 0.0;
+  for (int b = 0; b < g.nb; ++b) s += g.part[((int64_t)u * g.nb + b) * 3];
+  g.st[8 * u] = s;
+}
+
+__global__ void rho_init_kernel(GRhoArgs g, int32_t U) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < (int64_t)U * g.K) g.x[t] = 1.0;
+  if (t < U) {
+    double* st = g.st + 8 * t;
+    st[0] = (double)g.K; st[1] = 0.0; st[2] = -1.0; st[3] = 0.0; st[4] = 0.0; st[5] = 0.0; st[6] = 0.0; st[7] = 0.0;
+  }
+}
+
+__global__ void rho_out_kernel(GRhoArgs g, int32_t U, double* rho, int32_t* iters) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  const double* st = g.st + 8 * u;
+  rho[3 * u] = st[6] == 1.0 ? 0.5 * (st[3] + st[4]) : st[1];
+  rho[3 * u + 1] = st[3];
+  rho[3 * u + 2] = st[4];
+  iters[u] = (int32_t)st[7];
+}
+
+int spectral_radius_global(int32_t K, int32_t E, const double* d_a, const double* d_vals, const int32_t* d_cols,
+                           int32_t U, double tol, int32_t max_iter, double* d_rho, int32_t* d_iters,
+                           hipStream_t stream) {
+  GRhoArgs g{};
+  g.K = K; g.E = E; g.nb = (K + kGBlock - 1) / kGBlock;
+  g.a = d_a; g.vals = d_vals; g.cols = d_cols; g.tol = tol;
+  const size_t nx = (size_t)U * K;
+  HIP_CHECK(hipMallocAsync((void**)&g.x, sizeof(double) * (2 * nx + (size_t)U * g.nb * 3 + (size_t)U * 8), stream));
+  g.y = g.x + nx;
+  g.part = g.y + nx;
+  g.st = g.part + (size_t)U * g.nb * 3;
+  const unsigned ni = (unsigned)((std::max<size_t>(nx, (size_t)U) + 255) / 256);
+  hipLaunchKernelGGL(rho_init_kernel, dim3(ni), dim3(256), 0, stream, g, U);
+  std::vector<double> st((size_t)U * 8);
+  const dim3 grid((unsigned)g.nb, (unsigned)U);
+  const unsigned gu = (unsigned)((U + 255) / 256);
+  int rc = CVD_OK;
+  for (int it = 0; it < max_iter; ++it) {
+    hipLaunchKernelGGL(rho_matvec_kernel, grid, dim3(kGBlock), 0, stream, g);
+    hipLaunchKernelGGL(rho_step_kernel, dim3((unsigned)U), dim3(kGBlock), 0, stream, g);
+    hipLaunchKernelGGL(rho_scale_kernel, grid, dim3(kGBlock), 0, stream, g);
+    hipLaunchKernelGGL(rho_sum_kernel, dim3(gu), dim3(256), 0, stream, g, U);
+    if ((it & 31) == 31 || it + 1 == max_iter) {   // every u stopped?
+      if (hipMemcpyAsync(st.data(), g.st, sizeof(double) * st.size(), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+          hipStreamSynchronize(stream) != hipSuccess) {
+        cvd::set_error("spectral_radius: HIP error in the global iteration");
+        rc = CVD_E_HIP;
+        break;
+      }
+      bool all = true;
+      for (int u = 0; u < U && all; ++u) all = st[(size_t)u * 8 + 6] != 0.0;
+      if (all) break;
+    }
+  }
+  if (rc == CVD_OK) hipLaunchKernelGGL(rho_out_kernel, dim3(gu), dim3(256), 0, stream, g, U, d_rho, d_iters);
+  const hipError_t e = hipGetLastError();
+  (void)hipFreeAsync(g.x, stream);
+  if (rc == CVD_OK && e != hipSuccess) {
+    cvd::set_error(std::string("HIP error '") + hipGetErrorString(e) + "' in spectral_radius (global)");
+    rc = CVD_E_HIP;
+  }
+  return rc;
+}
+
 }  // namespace
 
 // ───────────────────────────────── ABI ──────────────────────────────────────
@@ -262,14 +449,21 @@ extern "C" int cvd_count_transitions(const cvd_model* model, const uint32_t* d_r
   const cvd_model& M = *model;
   if (M.kind != 0 || !M.d_rec) { cvd::set_error("count_transitions needs an enumerated (dense) model"); return CVD_E_UNSUPPORTED; }
   const int n = M.dec.n, R = 1 << n;
-  if (M.S >= 4096 || (n != 2 && n != 3)) {
-    cvd::set_error("count_transitions: S < 4096 and n in {2, 3}");
+  if (n != 2 && n != 3) {
+    cvd::set_error("count_transitions: n in {2, 3}");
     return CVD_E_UNSUPPORTED;
   }
   if (nseq == 0 || N == 0) return CVD_OK;
   CountArgs a;
   a.rec = M.d_rec; a.r = d_r; a.S = M.S; a.N = N; a.nseq = nseq; a.burn = burn_in; a.n = n;
   a.cnt = reinterpret_cast<unsigned long long*>(d_cnt);
+  if (M.S >= 4096) {   // 16-bit LDS records cannot hold the successor: records from L2
+    a.lds_hist = 0;
+    hipLaunchKernelGGL(n == 2 ? count_transitions_global_kernel<2> : count_transitions_global_kernel<3>,
+                       dim3((unsigned)((nseq + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+    HIP_CHECK(hipGetLastError());
+    return CVD_OK;
+  }
   const size_t SR = (size_t)M.S * R;
   a.lds_hist = SR * 6 <= 160 * 1024;
   const size_t lds = SR * 2 + (a.lds_hist ? SR * 4 : 0);
@@ -319,7 +513,12 @@ extern "C" int cvd_spectral_radius(int32_t K, int32_t E, const double* d_a, cons
     return CVD_E_INVALID;
   }
   const size_t lds = (size_t)2 * K * sizeof(double) + 16 * sizeof(double);
-  if (lds > 160 * 1024) { cvd::set_error("spectral_radius: K <= 10000 (two LDS vectors)"); return CVD_E_UNSUPPORTED; }
+  const char* force = std::getenv("CVD_RHO_GLOBAL");   // tests: the HBM path at small K
+  if (lds > 160 * 1024 || (force && force[0] == '1')) {
+    if (!d_cols) { cvd::set_error("spectral_radius: K > 10000 needs the structured (cols) form"); return CVD_E_UNSUPPORTED; }
+    if (U == 0) return CVD_OK;
+    return spectral_radius_global(K, E, d_a, d_vals, d_cols, U, tol, max_iter, d_rho, d_iters, (hipStream_t)stream);
+  }
   if (U == 0) return CVD_OK;
   RhoArgs p{K, E, d_a, d_vals, d_cols, tol, max_iter, d_rho, d_iters};
   if (lds > 64 * 1024)
