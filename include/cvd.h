@@ -192,7 +192,8 @@ int cvd_chernoff_build_dense(int32_t K, int32_t R, const double* d_P1, const dou
  * by power iteration with Collatz-Wielandt bounds: d_rho[3u..3u+2] = (estimate,
  * lower, upper bound) once (upper - lower) <= tol * upper (irreducible M), else
  * once the power-iteration norm ratio is stable to tol/100 (the estimate), or
- * after max_iter iterations (d_iters[u]).  K <= 10000. */
+ * after max_iter iterations (d_iters[u]).  K <= 10000: vectors in LDS, one workgroup per u;
+ * larger K (structured form only, d_cols non-NULL): vectors in HBM, one launch per phase. */
 int cvd_spectral_radius(int32_t K, int32_t E, const double* d_a, const double* d_vals,
                         const int32_t* d_cols, int32_t U, double tol, int32_t max_iter, double* d_rho,
                         int32_t* d_iters, void* stream);

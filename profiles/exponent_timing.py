@@ -25,6 +25,8 @@ CASES = {
                          [[0, 1, 1, 0, 0], [1, 1, 0, 1, 0]]],
                [[[1, 1, 1, 0, 1], [0, 1, 0, 1, 0]], [[0, 1, 1, 0, 0], [1, 1, 0, 1, 0]],
                 [[1, 0, 0, 0, 1], [0, 1, 1, 1, 1]]]),
+    # K = 150,743: the HBM power iteration (above the LDS limit)
+    "m4": (1, 2, 4, [[[1, 0, 0, 1, 1]], [[1, 1, 1, 0, 1]]], [[[1, 1, 1, 0, 1]], [[1, 0, 0, 1, 1]]]),
 }
 
 
