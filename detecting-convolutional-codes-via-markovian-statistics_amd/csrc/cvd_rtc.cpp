@@ -85,11 +85,17 @@ bool compile_clang(const std::string& src, const std::string& arch, std::vector<
   const std::string arch_opt = "--offload-arch=" + arch;
   std::vector<std::string> args = {clang, "-x", "hip", arch_opt, "--offload-device-only", "--no-gpu-bundle-output",
                                    "-O3", "-std=c++17", "-ffp-contract=off", "-c", in, "-o", out};
-  if (const char* d = std::getenv("CVD_JIT_DEFINES")) {   // tuning experiments: extra -D options only
+  if (const char* d = std::getenv("CVD_JIT_DEFINES")) {   // tuning experiments: -D and -mllvm <opt> only
     std::istringstream ds(d);
-    std::string t;
-    while (ds >> t)
-      if (t.rfind("-D", 0) == 0) args.insert(args.end() - 4, t);
+    std::string t, o;
+    while (ds >> t) {
+      if (t.rfind("-D", 0) == 0) {
+        args.insert(args.end() - 4, t);
+      } else if (t == "-mllvm" && ds >> o) {
+        args.insert(args.end() - 4, t);
+        args.insert(args.end() - 4, o);
+      }
+    }
   }
   std::vector<char*> argv;
   for (auto& s : args) argv.push_back(&s[0]);

@@ -32,8 +32,8 @@ def main():
         i = args.index("--isa")
         isa = args[i + 1]
         del args[i:i + 2]
-    defs = [x for x in args if x.startswith("-D")]
-    rest = [x for x in args if not x.startswith("-D")]
+    defs = [x for x in args if x.startswith("-")]   # -D... and -mllvm pairs (as CVD_JIT_DEFINES)
+    rest = [x for x in args if not x.startswith("-")]
     m, xm = code_constant(rest[0] if rest else "m6")
     clang = os.environ.get("CVD_JIT_CLANG", "/opt/rocm/lib/llvm/bin/clang++")
     with tempfile.TemporaryDirectory() as d:
