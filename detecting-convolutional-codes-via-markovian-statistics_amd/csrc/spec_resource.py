@@ -43,7 +43,8 @@ def main():
                     'extern "C" __global__ __launch_bounds__(cvd_dev::kBlock, cvd_dev::kK1bWavesPerSimd)\n'
                     f'void cvd_k1b_spec(cvd_dev::ExpArgs a) {{ cvd_dev::k1b_body<{m}, true, 0x{xm:016x}ull, false>(a); }}\n')
         base = [clang, "-x", "hip", "--offload-arch=gfx950", "--offload-device-only", "--no-gpu-bundle-output",
-                "-O3", "-std=c++17", "-ffp-contract=off", "-I", HERE, *defs]
+                "-O3", "-std=c++17", "-ffp-contract=off", "-mllvm", "--amdgpu-sched-strategy=max-ilp",
+                "-I", HERE, *defs]
         r = subprocess.run(base + ["-Rpass-analysis=kernel-resource-usage", "-c", src, "-o",
                                    os.path.join(d, "k.co")], capture_output=True, text=True)
         for line in r.stderr.splitlines():
