@@ -103,10 +103,10 @@ def main():
         models = {p: det.model(p, a.learn_len if m == 6 else None, 200, 1.0, a.seed) for p in p_grid}
         info = models[p_grid[0]].info()
     # whole residency rounds: 4 waves/SIMD x 1024 SIMDs x 64 lanes = 262,144 sequences
-    # (131,072 trials) per round.  m6: 10 rounds per launch (65.5 GB of streams) -- the
+    # (131,072 trials) per round.  m6: 20 rounds per launch (131 GB of streams) -- the
     # last round's uneven wave finish costs ~24 ms per launch, amortised over the rounds
-    # (profiles/ab_k1b.py: 1.227 us/trial at 2 rounds, 1.173 at 5)
-    B = a.batch or {"m6": 1_310_720, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
+    # (DESIGN.md "Launch size": 687k trials/s at 2 rounds, 735k at 10, 742k at 20)
+    B = a.batch or {"m6": 2_621_440, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
     # double-buffered pipeline: the generator fills buffer (s+1)%2 on its own
     # stream while the detector reads buffer s%2 (both kernels of every timed
     # step run inside the timed region)
