@@ -346,3 +346,25 @@ def test_m6_headline_config_sums_vs_c_oracle(pkg, dev, p):
         cnt, want = cm.run_trials(c1, c2, N, p, seed, t0, t1, sums=True)
         assert np.array_equal(got["sums"], want)
         assert tuple(got["counts"].cpu().tolist()) == tuple(int(x) for x in cnt)
+
+
+def test_m6_batch_beyond_32bit_offsets(pkg, dev):
+    """One launch over a 35 GB stream buffer (dword offsets past 2^32): the sums of
+    the last trials, whose words sit at the highest offsets, equal the C oracle's."""
+    from oracle import c_oracle as C
+    cc = pkg.CONFIG_CODES["m6"]
+    N, p, seed, B = 100_000, 0.05, 12345, 700_000
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    model = det.model(p, 200_000, 200, 1.0, seed)
+    assert det.words_per_seq(N) * 2 * B > (1 << 32)
+    tag = pkg.grid_tag(N, p)
+    r = det.stream_buffer(N, 2 * B)
+    det.generate(cc["gen1"], N, p, seed, tag, 0, 2, B, out=r, q0=0, pitch=2 * B)
+    det.generate(cc["gen2"], N, p, seed, tag, 1, 2, B, out=r, q0=B, pitch=2 * B)
+    sums = torch.empty((2 * B, 2), dtype=torch.float64, device=r.device)
+    det.detect(model, r, N, 2 * B, B, sums=sums)
+    s = sums[torch.tensor([B - 2, B - 1, 2 * B - 2, 2 * B - 1], device=r.device)].cpu().numpy()
+    del r, sums
+    c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
+    _, want = C.Model(c1, p, 200_000, 200, 1.0, seed).run_trials(c1, c2, N, p, seed, B - 2, B, sums=True)
+    assert np.array_equal(s[:2], want[:, :2]) and np.array_equal(s[2:], want[:, 2:])
