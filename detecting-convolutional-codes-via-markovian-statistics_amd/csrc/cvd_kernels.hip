@@ -311,13 +311,18 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
             uint32_t o = 0u;
 #pragma unroll
             for (int r = 0; r < k; ++r) {
-              // the tap mask is re-read per word: hoisted out of the chunk loop, its
-              // per-shift branch conditions fill the SGPRs (spills through v_writelane)
+              // the set taps only, as a scalar loop over the uniform mask (s_ff1):
+              // two VALU per tap.  The mask is re-read per word -- hoisted out of
+              // the chunk loop, per-shift conditions filled the SGPRs (spills) and
+              // unrolled they became selects for every possible shift
               uint32_t tm = a.taps[j][r];
               asm volatile("" : "+s"(tm));
-#pragma unroll
-              for (int sh = 0; sh <= kMaxM; ++sh)
-                if ((tm >> sh) & 1u) o ^= Wr[r] >> sh;
+#pragma nounroll
+              while (tm) {
+                const uint32_t sh = (uint32_t)__builtin_ctz(tm);
+                tm &= tm - 1u;
+                o ^= Wr[r] >> sh;
+              }
             }
             if constexpr (SPW < 32) o &= (1u << SPW) - 1u;
             word |= spread_n<n>(o) << j;
