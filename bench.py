@@ -100,7 +100,7 @@ def main():
         tpl = pkg.default_template(cc["gen1"], m)
         models, info = {}, {"kind": 0, "explicit_kernel": 0, "learn_len_eff": 0, "n_rows": 0}
     else:
-        models = {p: det.model(p, a.learn_len if m == 6 else None, 200, 1.0, a.seed) for p in p_grid}
+        models = dict(zip(p_grid, det.prepare_models(p_grid, a.learn_len if m == 6 else None, 200, 1.0, a.seed)))
         info = models[p_grid[0]].info()
     # whole residency rounds: 4 waves/SIMD x 1024 SIMDs x 64 lanes = 262,144 sequences
     # (131,072 trials) per round.  m6: 20 rounds per launch (131 GB of streams) -- the

@@ -138,6 +138,26 @@ class Detector:
             self._models.popitem(last=False)
         return mod
 
+    def prepare_models(self, p_list, learn_len=None, learn_burn=200, laplace=1.0, seed=12345, workers=None):
+        """Learn the models of several p at once (host threads; cvd_model_create
+        runs without the GIL), then upload them in order.  The learning chain of
+        one model is sequential, so a p sweep's setup costs about its slowest
+        model instead of the sum."""
+        from concurrent.futures import ThreadPoolExecutor
+        keys = {}
+        for p in p_list:
+            key = (float(p), learn_len, int(learn_burn), float(laplace), int(seed))
+            if key not in self._models:
+                keys[key] = float(p)
+        if len(keys) > 1:
+            nw = workers or min(len(keys), 8)
+            with ThreadPoolExecutor(max_workers=nw) as ex:
+                built = list(ex.map(lambda p: Model(self.dec, p, learn_len, learn_burn, laplace, seed,
+                                                    self.enum_cap, self.default_learn_len), keys.values()))
+            for key, mod in zip(keys, built):
+                self._models[key] = mod.upload(self.device.index)
+        return [self.model(p, learn_len, learn_burn, laplace, seed) for p in p_list]
+
     def words_per_seq(self, N):
         """Received words per sequence, padded to whole 16-byte chunks."""
         spw = 32 // self.n
@@ -258,6 +278,8 @@ def run_experiment(k, n, m, gen1, gen2, num_iter, p_vec, learn_len, learn_burn, 
 
     det = _detector(k, n, m, gen1, device)
     N_spectrum = list(N_SPECTRUM_BY_M.get(m, [50, 100, 200]) if N_list is None else N_list)
+
+    det.prepare_models(list(p_vec), learn_len, learn_burn, laplace, seed)
 
     def count_fn(iN, N, ip, p, lo, hi, out):
         model = det.model(p, learn_len, learn_burn, laplace, seed)

@@ -81,3 +81,19 @@ def test_c_oracle_sparse_sums_vs_python(pkg):
                 lr += math.log(c / 4)
                 D = succ[rv]
             assert sums[t - 10, 2 * hyp] == lp and sums[t - 10, 2 * hyp + 1] == lr
+
+
+def test_models_learned_in_parallel_equal_sequential(pkg):
+    """Models of a p sweep learned on concurrent host threads (Detector.prepare_models)
+    are identical to sequentially learned ones (host only, no upload)."""
+    from concurrent.futures import ThreadPoolExecutor
+    cc = pkg.CONFIG_CODES["m6"]
+    dec = pkg.Code(cc["gen1"], 6, 1, 2)
+    ps = [0.02, 0.1, 0.2]
+    seq = [pkg.Model(dec, p, 20000, 200, 1.0, 7) for p in ps]
+    with ThreadPoolExecutor(3) as ex:
+        par = list(ex.map(lambda p: pkg.Model(dec, p, 20000, 200, 1.0, 7), ps))
+    for a, b in zip(seq, par):
+        la, ka = a.rows()
+        lb, kb = b.rows()
+        assert np.array_equal(la, lb) and np.array_equal(ka, kb)
