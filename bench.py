@@ -253,7 +253,9 @@ def main():
                        "per_p": per_p},
     }
     if a.cpu_baseline and world == 1 and not parity:
-        out["cpu_baseline"] = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds)
+        out["cpu_baseline"], cpu_check = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds)
+        if 0.05 in models:
+            out["pd_match_vs_cpu"] = pd_match(det, models[0.05], cc, N, a.seed, cpu_check)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -269,16 +271,32 @@ def cpu_baseline(cc, k, n, m, N, seed, learn_len, seconds):
     mod = C.Model(c1, p, learn_len if m == 6 else None, 200, 1.0, seed)
     # calibrate with one trial per thread, then size the sample to ~`seconds`
     t0 = time.perf_counter()
-    mod.run_trials(c1, c2, N, p, seed, 0, threads, nthreads=threads)
+    c_cal, s_cal = mod.run_trials(c1, c2, N, p, seed, 0, threads, sums=True, nthreads=threads)
     dt = time.perf_counter() - t0
     ntr = max(threads, int(threads * seconds / max(dt, 1e-6)) // threads * threads)
     t0 = time.perf_counter()
-    mod.run_trials(c1, c2, N, p, seed, threads, threads + ntr, nthreads=threads)
+    c_smp, _ = mod.run_trials(c1, c2, N, p, seed, threads, threads + ntr, nthreads=threads)
     dt = time.perf_counter() - t0
+    check = {"p": p, "trials": threads + ntr, "counts": [int(x) for x in c_cal + c_smp], "sums": s_cal}
     return {"value": ntr / dt, "unit": "trials/s", "cores": threads, "kind": "port",
             "sample": f"{ntr} trials (H1+H2, N={N}) at p={p}, C oracle (oracle/cvd_oracle.c), "
                       f"{threads} OpenMP threads, {dt:.1f} s",
-            "seconds": dt}
+            "seconds": dt}, check
+
+
+def pd_match(det, model, cc, N, seed, check):
+    """The metric's "Pd match vs CPU": the GPU path on the CPU sample's trial ids
+    (same model, same streams) -- success counts equal, and the per-trial fp64
+    log-likelihood sums of the calibration trials bit-identical.  Outside the
+    timed region."""
+    T, p = check["trials"], check["p"]
+    got = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 0, T)["counts"].cpu().tolist()
+    ncal = len(check["sums"])
+    sums = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 0, ncal, return_sums=True)["sums"]
+    same_sums = bool(np.array_equal(sums, check["sums"]))
+    return {"p": p, "trials": T, "gpu_counts": got, "cpu_counts": check["counts"],
+            "pd_gpu": got[0] / T, "pd_cpu": check["counts"][0] / T,
+            "sums_bit_exact_trials": ncal, "match": got == check["counts"] and same_sums}
 
 
 if __name__ == "__main__":
