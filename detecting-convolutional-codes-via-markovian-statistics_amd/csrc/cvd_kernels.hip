@@ -280,9 +280,9 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
             uint32_t xv[kPG][4];
 #pragma unroll
             for (int gb = 0; gb < kPG; ++gb) {
-              const U4 x = philox(b0 + (uint32_t)(g0 + gb), slo, nhi, a.tag, k0, k1);
-              xv[gb][0] = x.x; xv[gb][1] = x.y; xv[gb][2] = x.z; xv[gb][3] = x.w;
+              xv[gb][0] = b0 + (uint32_t)(g0 + gb); xv[gb][1] = slo; xv[gb][2] = nhi; xv[gb][3] = a.tag;
             }
+            philox_blocks<kPG>(xv, k0, k1);
 #pragma unroll
             for (int gb = kPG - 1; gb >= 0; --gb)
 #pragma unroll
