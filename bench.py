@@ -106,7 +106,8 @@ def main():
     # (131,072 trials) per round.  m6: 20 rounds per launch (131 GB of streams) -- the
     # last round's uneven wave finish costs ~24 ms per launch, amortised over the rounds
     # (DESIGN.md "Launch size": 687k trials/s at 2 rounds, 735k at 10, 742k at 20)
-    B = a.batch or {"m6": 2_621_440, "m2": 1_048_576, "r23_m4": 131_072}[a.config]
+    # m2: 2^22 trials (56.0M vs 52.3M trials/s at 2^20); r23_m4: 2^17 measured best
+    B = a.batch or {"m6": 2_621_440, "m2": 4_194_304, "r23_m4": 131_072}[a.config]
     # double-buffered pipeline: the generator fills buffer (s+1)%2 on its own
     # stream while the detector reads buffer s%2 (both kernels of every timed
     # step run inside the timed region)
