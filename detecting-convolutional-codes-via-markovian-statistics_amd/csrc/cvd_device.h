@@ -221,12 +221,18 @@ struct RowCursor {
     return d == 0u;
   }
   // log P̂1(row(D_{t-1}), r); afterwards `slot` describes row(D_t)
-  __device__ double resolve(const ExpArgs& a, const uint32_t (&key)[NW], uint32_t r) {
+  // kmu8: the stored key is the canonical key + kmu8 in every nibble (lazy
+  // normalisation, CVD_K1B_LAZYKEY); subtracted only where the key is compared
+  // or hashed
+  __device__ double resolve(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t r, uint32_t kmu8 = 0u) {
     double lpv = a.lp_unseen;
     int32_t ns = -2;
     if (slot >= 0) {
       lpv = plp; ns = pnx;
     } else if (cand) {
+      uint32_t key[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) key[w] = key_in[w] - kmu8;
       if (same_key(pkey, key)) {
         lpv = plp; ns = pnx;
       } else if (pkey[0] != kEmptyKey) {
@@ -251,10 +257,13 @@ struct RowCursor {
     return lpv;
   }
   // D_t's key is known: issue the next step's loads
-  __device__ void prefetch(const ExpArgs& a, const uint32_t (&key)[NW], uint32_t rn) {
+  __device__ void prefetch(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t rn, uint32_t kmu8 = 0u) {
     if (slot >= 0) {
       prefetch_row(a, slot, rn);
     } else if (slot == -2) {
+      uint32_t key[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) key[w] = key_in[w] - kmu8;
       uint32_t h1, h2;
       key_hash(key, NW, h1, h2);
       hs = h1 & a.hmask;
@@ -311,6 +320,9 @@ __device__ __forceinline__ void k1b_trace(uint8_t* tr, int64_t t, int64_t nseq, 
 #endif
 #ifndef CVD_K1B_MID
 #define CVD_K1B_MID 2
+#endif
+#ifndef CVD_K1B_LAZYKEY
+#define CVD_K1B_LAZYKEY 0
 #endif
 constexpr int kK1bWavesPerSimd = CVD_K1B_WAVES;
 constexpr int kRenorm = 128;   // O <= 128: raw pair values stay < 256 (byte packing)
@@ -456,6 +468,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
 #pragma unroll
     for (int w = 0; w < NW; ++w) key[w] = 0u;
     uint32_t O = 0u, O8 = 0u;   // O8 = O * 0x11111111
+    uint32_t kmu8 = 0u;         // nibble offset of the stored key (lazy normalisation)
     if constexpr (kTrace) k1b_trace<m>(a.trace, 0, a.nseq, qwave + lane_id(), key);
     // Received words: word w of this sequence at rbase + (w/4)*cstride + w%4
     // (16-byte chunks, include/cvd.h).  Only the current word and the next are
@@ -492,7 +505,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       // P̂1 row of D_{t-1}
       cur.fence(zn);                          // zn depends on the whole ACS
       cur.template fence_keys<NW>(zn);
-      lp += cur.resolve(a, key, rr);          // Pd_plotter.py:115, T = P̂1
+      lp += cur.resolve(a, key, rr, kmu8);    // Pd_plotter.py:115, T = P̂1
       // halves differences of D_{t-1}: nibble of state j (< 2^(m-1)) is nonzero
       // iff D_{t-1}(j) != D_{t-1}(j + 2^(m-1))
       constexpr int NH = NW >= 2 ? NW / 2 : 1;
@@ -512,13 +525,22 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
         hx |= dh[v];
         sym |= dh[v] & (a.bfly_even[v] ^ pm);
       }
+      // D_t's key.  Lazy form: raw nibbles (canonical + mu in every nibble, no
+      // borrow since mu = 1 means every nibble >= 1); the halves test only asks
+      // which nibbles are equal, which the common offset leaves unchanged
 #pragma unroll
-      for (int v = 0; v < NW; ++v) key[v] = kw[v] - mu8;
+      for (int v = 0; v < NW; ++v) key[v] = CVD_K1B_LAZYKEY ? kw[v] : kw[v] - mu8;
+      kmu8 = CVD_K1B_LAZYKEY ? mu8 : 0u;
       // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni
       const uint32_t c = 1u + (sym == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
       lr += s_lt[c];                          // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
-      if constexpr (kTrace) k1b_trace<m>(a.trace, t, a.nseq, qwave + lane_id(), key);
-      cur.prefetch(a, key, rn);
+      if constexpr (kTrace) {
+        uint32_t ck[NW];
+#pragma unroll
+        for (int v = 0; v < NW; ++v) ck[v] = key[v] - kmu8;
+        k1b_trace<m>(a.trace, t, a.nseq, qwave + lane_id(), ck);
+      }
+      cur.prefetch(a, key, rn, kmu8);
     };
 
     // groups of 4 steps (a quarter word): the 10 bits they read (4 words and
