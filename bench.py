@@ -10,32 +10,56 @@ Pd_plotter.py:210-223).  One step = one batch of `--batch` trials per GPU at
 one p of the sweep (step s uses p_grid[s % 6]): the generator kernel writes the
 batch's BSC-noised received streams to HBM (encoder + Philox noise, two
 launches: H1 with G1, H2 with G2), then the detector kernel reads them
-(Eq. 4-5 recursion for all 2^n received words, T_ref count, hashed P̂1 row
-lookup, fp64 log-likelihood sums, decisions, counts).  Both kernels are inside
-the timed region; learning P̂1 (host setup, once per p) is not.
+(Eq. 4-5 recursion, T_ref count, hashed P̂1 row lookup, fp64 log-likelihood
+sums, decisions, counts).  Both kernels are inside the timed region; learning
+P̂1 (host setup, once per p) is not.
 
-Multi-GPU (torchrun): one process per GPU, rank r takes its own global trial
-ids every step (weak scaling); the success counts are reduced with one RCCL
-all_reduce at the end of the timed region.
+Multi-GPU: one process per GPU, rank r takes its own global trial ids every
+step (weak scaling); the success counts are reduced with one RCCL all_reduce
+at the end of the timed region.  `--gpus N` without a torch.distributed
+launcher (no WORLD_SIZE in the environment) starts the N ranks itself, before
+any GPU call, and exits with their status; under a launcher WORLD_SIZE must
+equal --gpus.
+
+After the timed region (rank 0, one GPU): the CPU baseline (the C oracle on
+this host's cores), the "Pd match vs CPU" check at the config's informative
+grid point (where Pd is neither 0 nor 1: exact counts on shared trial ids plus
+a 3-sigma binomial test against a large independent GPU sample), and the C0
+demo preset run in full on both sides.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-from __graft_entry__ import load_package  # noqa: E402
 
 METRIC = "MC trials/sec at N=1e5, rate-1/2 m=6 pair, 1/2/4/8 GPUs; Pd match vs CPU"
 P_GRID = [0.01, 0.02, 0.05, 0.10, 0.15, 0.20]
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
+VALU_PEAK_WINST = 1024 * 2.4e9 / 2
+
+# Informative grid points (Pd neither 0 nor 1) at each config's own N, found with the
+# C oracle (profiles/pd_points.jsonl): the headline sweep's Pd is 0 for m = 6 (the
+# reference estimator's S*laplace denominator, DESIGN.md D4), so the Pd match runs here.
+PD_POINTS = {
+    "m6": {"N": 100_000, "p": 0.0033, "learn_len": 10_000_000},     # Pd ~ 0.27
+    "m2": {"N": 10_000, "p": 0.092, "learn_len": None},             # Pd ~ 0.57
+    "r23_m4": {"N": 100_000, "p": 0.0135, "learn_len": None},       # Pd ~ 0.33
+}
+# C0: demo_script.py preset 1 as BASELINE.json configs[0] states it -- (7,5) vs (5,7),
+# m = 2, N = 1e3, 1e3 trials, the demo's p grid and seed (demo_script.py:114-131)
+C0 = {"gen1": [[[1, 1, 1]], [[1, 0, 1]]], "gen2": [[[1, 0, 1]], [[1, 1, 1]]], "N": 1000, "trials": 1000,
+      "p_vec": [0.01, 0.05, 0.1, 0.2, 0.3], "seed": 123}
 
 
 def parse():
@@ -59,17 +83,53 @@ def parse():
     ap.add_argument("--overlap", type=int, default=-1,
                     help="generate the next batch on a second stream while the detector runs "
                          "(-1: auto = on for the table automaton, where it measured faster)")
-    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle port (rank 0, N=1)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-baseline", type=int, default=1,
+                    help="time the C oracle port on this host (rank 0, one GPU), check Pd against it at "
+                         "the config's informative point, and run the C0 demo preset on both sides")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work per timed CPU sample")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="C oracle threads (default: the host CPUs this process may run on, capped by "
+                         "OMP_NUM_THREADS when set -- the GPU box's CPU share)")
     ap.add_argument("--pmc-traffic", default=None,
-                    help="per-launch detector FETCH_SIZE summary of a rocprofv3 --pmc pass "
+                    help="per-launch detector counter summary of rocprofv3 --pmc passes "
                          "(profiles/collect.sh + summarize.py; default profiles/pmc_<detector>_<config>.json); "
                          "used only when its config/batch/N match this run")
     return ap.parse_args()
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a):
+    """`--gpus N` without a launcher: start N ranks (torch.distributed.run, one
+    process per GPU) as children before this process touches the GPU, and
+    return their exit status.  Under a launcher, check WORLD_SIZE == --gpus."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != a.gpus:
+            print(json.dumps({"error": f"WORLD_SIZE={world_env} but --gpus {a.gpus}"}), flush=True)
+            sys.exit(2)
+        return None
+    if a.gpus <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     a = parse()
+    rc = launch_ranks(a)
+    if rc is not None:
+        sys.exit(rc)
+    import numpy as np
+    import torch
+    from __graft_entry__ import load_package
     pkg = load_package()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -95,6 +155,7 @@ def main():
     g1 = pkg.Code(cc["gen1"], m, k, n)
     g2 = pkg.Code(cc["gen2"], m, k, n)
     parity = a.detector == "parity"
+    t_setup = time.perf_counter()
     if parity:
         # parity-template baseline (comp_parity.py): template of G1, no learned model
         tpl = pkg.default_template(cc["gen1"], m)
@@ -102,6 +163,7 @@ def main():
     else:
         models = dict(zip(p_grid, det.prepare_models(p_grid, a.learn_len if m == 6 else None, 200, 1.0, a.seed)))
         info = models[p_grid[0]].info()
+    t_setup = time.perf_counter() - t_setup
     # whole residency rounds: 4 waves/SIMD x 1024 SIMDs x 64 lanes = 262,144 sequences
     # (131,072 trials) per round.  m6: 20 rounds per launch (131 GB of streams) -- the
     # last round's uneven wave finish costs ~24 ms per launch, amortised over the rounds
@@ -168,6 +230,7 @@ def main():
                 ready[s + 1].record(gstream)
         dstream.wait_stream(gstream)
 
+    # warmup steps use trial ids far from the timed ones (base 10,000 steps)
     run(a.warmup, 10_000)
     counts.zero_()
     torch.cuda.synchronize()
@@ -186,6 +249,8 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         t = torch.tensor([elapsed], device=det.device, dtype=torch.float64)
+        if a.dist_backend == "gloo":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gen_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
@@ -202,17 +267,29 @@ def main():
     # received streams read once, 2 * ceil(N * n / 8) bytes per trial
     alg_bytes = B * 2 * ((N * n + 7) // 8)
     achieved = alg_bytes / (det_ms * 1e-3) / 1e9
-    traffic, traffic_src, valu = None, None, None
+    traffic, traffic_src, pmc = None, None, None
     if a.pmc_traffic is None:
         a.pmc_traffic = os.path.join(ROOT, "profiles", f"pmc_{a.detector}_{a.config}.json")
     if a.pmc_traffic and os.path.exists(a.pmc_traffic):
         with open(a.pmc_traffic) as f:
             pmc = json.load(f)
-        if (pmc.get("config"), pmc.get("batch"), pmc.get("N"), pmc.get("detector", "markov")) == \
+        if (pmc.get("config"), pmc.get("batch"), pmc.get("N"), pmc.get("detector", "markov")) != \
                 (a.config, B, N, a.detector):
-            traffic = pmc.get("detector_fetch_bytes_per_launch")
-            valu = {k: pmc.get(k) for k in ("VALU_insts_per_wave_step", "valu_issue_frac_est", "kernel")}
-            traffic_src = os.path.relpath(a.pmc_traffic, ROOT) + " (rocprofv3 FETCH_SIZE x1024 x2, gfx950 correction)"
+            pmc = None
+    valu = None
+    if pmc is not None:
+        traffic = pmc.get("detector_fetch_bytes_per_launch")
+        traffic_src = os.path.relpath(a.pmc_traffic, ROOT) + " (" + pmc.get("traffic_basis", "rocprofv3 FETCH_SIZE") + ")"
+        ipws = pmc.get("VALU_insts_per_wave_step")
+        if ipws:
+            # VALU roofline of the detector (its binding resource): wave-instructions
+            # per launch from the counter pass, over this run's live launch time
+            winst = ipws * (2 * B / 64) * N
+            ach = winst / (det_ms * 1e-3)
+            valu = {"insts_per_wave_step": ipws, "achieved": ach, "peak": VALU_PEAK_WINST,
+                    "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WINST,
+                    "issue_cycle_weighted_frac": pmc.get("valu_issue_cycle_frac"),
+                    "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU) + live HIP-event time"}
     c = counts.cpu().numpy()
     per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, (a.steps // len(p_grid) + (i < a.steps % len(p_grid))) * B * world),
                       "h1_successes": int(c[i, 0]), "h2_successes": int(c[i, 1])}
@@ -237,67 +314,170 @@ def main():
                    "trials_per_step_per_gpu": B, "model": info["kind"] and "sparse(learned)" or "dense",
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "roofline": {"bound": "valu" if valu else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("parity_kernel (parity-template baseline, cvd_parity.hip)" if parity
                                 else pkg.KERNEL_NAMES[info["explicit_kernel"]] if info["kind"]
                                 else "detect_table_kernel (enumerated state automaton)"),
                      "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms},
+                     "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms,
+                     "valu": valu},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
-                       "overlap": bool(a.overlap),
+                       "overlap": bool(a.overlap), "model_setup_s": t_setup,
                        "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
                        "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
                        "detector_ms_steps": det_each,
-                       # the binding resource is VALU issue, not HBM: from the PMC summary
-                       "valu_bound": valu,
                        "per_p": per_p},
     }
     if a.cpu_baseline and world == 1 and not parity:
-        out["cpu_baseline"], cpu_check = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds)
-        if 0.05 in models:
-            out["pd_match_vs_cpu"] = pd_match(det, models[0.05], cc, N, a.seed, cpu_check)
+        host = host_info(a.cpu_threads)
+        out["cpu_baseline"], _ = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds, host)
+        out["pd_match_vs_cpu"] = pd_match(pkg, det, cc, a.config, k, n, m, a.seed, a.cpu_seconds, host)
+        out["c0_demo"] = c0_demo(pkg, host)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline(cc, k, n, m, N, seed, learn_len, seconds):
+def host_info(threads=None):
+    """The host cores the CPU legs use: every CPU this process may run on, capped by
+    OMP_NUM_THREADS when set (the GPU box exports its CPU share there; os.cpu_count()
+    reports the whole machine)."""
+    allowed = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if threads:
+        use = threads
+    elif omp and omp.isdigit() and int(omp) > 0:
+        use = min(allowed, int(omp))
+    else:
+        use = allowed
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"threads": int(use), "host_logical_cpus": os.cpu_count(), "affinity_cpus": allowed,
+            "omp_num_threads_env": omp, "cpu_model": model}
+
+
+def _sized_sample(run, threads, seconds, cal_trials):
+    """Calibrate with `cal_trials`, then size a sample to ~`seconds` of CPU work (whole
+    multiples of the thread count).  Returns the sample's trial count."""
+    t0 = time.perf_counter()
+    run(0, cal_trials)
+    dt = max(time.perf_counter() - t0, 1e-6)
+    ntr = max(threads, int(cal_trials * seconds / dt) // threads * threads)
+    return ntr
+
+
+def cpu_baseline(cc, k, n, m, N, seed, learn_len, seconds, host):
     """The oracle's C port of the reference path (oracle/cvd_oracle.c), OpenMP over
-    trials on this host's cores, on a bounded sample of the same workload."""
+    trials on this host's cores, on a bounded sample of the headline workload (p = 0.05)."""
     from oracle import c_oracle as C
-    threads = min(16, os.cpu_count() or 1)
+    threads = host["threads"]
     c1, c2 = C.Code(cc["gen1"], m, k, n), C.Code(cc["gen2"], m, k, n)
     p = 0.05
     mod = C.Model(c1, p, learn_len if m == 6 else None, 200, 1.0, seed)
-    # calibrate with one trial per thread, then size the sample to ~`seconds`
+    ntr = _sized_sample(lambda lo, hi: mod.run_trials(c1, c2, N, p, seed, lo, hi, nthreads=threads),
+                        threads, seconds, threads)
     t0 = time.perf_counter()
-    c_cal, s_cal = mod.run_trials(c1, c2, N, p, seed, 0, threads, sums=True, nthreads=threads)
+    c_smp, _ = mod.run_trials(c1, c2, N, p, seed, 0, ntr, nthreads=threads)
     dt = time.perf_counter() - t0
-    ntr = max(threads, int(threads * seconds / max(dt, 1e-6)) // threads * threads)
-    t0 = time.perf_counter()
-    c_smp, _ = mod.run_trials(c1, c2, N, p, seed, threads, threads + ntr, nthreads=threads)
-    dt = time.perf_counter() - t0
-    check = {"p": p, "trials": threads + ntr, "counts": [int(x) for x in c_cal + c_smp], "sums": s_cal}
     return {"value": ntr / dt, "unit": "trials/s", "cores": threads, "kind": "port",
-            "sample": f"{ntr} trials (H1+H2, N={N}) at p={p}, C oracle (oracle/cvd_oracle.c), "
-                      f"{threads} OpenMP threads, {dt:.1f} s",
-            "seconds": dt}, check
+            "sample": f"{ntr} trials (H1+H2, N={N}) at p={p} of the headline sweep, C oracle "
+                      f"(oracle/cvd_oracle.c, OpenMP), {threads} threads, {dt:.1f} s",
+            "seconds": dt, "host": host}, [int(x) for x in c_smp]
 
 
-def pd_match(det, model, cc, N, seed, check):
-    """The metric's "Pd match vs CPU": the GPU path on the CPU sample's trial ids
-    (same model, same streams) -- success counts equal, and the per-trial fp64
-    log-likelihood sums of the calibration trials bit-identical.  Outside the
-    timed region."""
-    T, p = check["trials"], check["p"]
-    got = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 0, T)["counts"].cpu().tolist()
-    ncal = len(check["sums"])
+def pd_match(pkg, det, cc, config, k, n, m, seed, seconds, host):
+    """The metric's "Pd match vs CPU" at the config's informative grid point
+    (Pd neither 0 nor 1; PD_POINTS).  Outside the timed region.
+
+    (1) exact: the GPU path on the CPU sample's own trial ids (same learned model,
+        same streams) gives the same success counts, and the per-trial fp64
+        log-likelihood sums of the first trials are bit-identical;
+    (2) statistical: Pd of a large independent GPU sample (other trial ids) agrees
+        with the CPU sample's Pd within 3 binomial standard deviations of the
+        difference (pooled Pd).  Pc is checked the same way."""
+    from oracle import c_oracle as C
+    import numpy as np
+    pt = PD_POINTS[config]
+    N, p, ll = pt["N"], pt["p"], pt["learn_len"]
+    threads = host["threads"]
+    t0 = time.perf_counter()
+    c1, c2 = C.Code(cc["gen1"], m, k, n), C.Code(cc["gen2"], m, k, n)
+    cm = C.Model(c1, p, ll, 200, 1.0, seed)
+    t_cpu_learn = time.perf_counter() - t0
+    ntr = _sized_sample(lambda lo, hi: cm.run_trials(c1, c2, N, p, seed, lo, hi, nthreads=threads),
+                        threads, seconds, threads)
+    ntr = max(ntr, 64)
+    t0 = time.perf_counter()
+    c_cpu, _ = cm.run_trials(c1, c2, N, p, seed, 0, ntr, nthreads=threads)
+    t_cpu = time.perf_counter() - t0
+    ncal = min(16, ntr)
+    _, s_cpu = cm.run_trials(c1, c2, N, p, seed, 0, ncal, sums=True, nthreads=threads)
+    t0 = time.perf_counter()
+    model = det.model(p, ll, 200, 1.0, seed)
+    t_gpu_learn = time.perf_counter() - t0
+    got = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 0, ntr)["counts"].cpu().tolist()
     sums = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 0, ncal, return_sums=True)["sums"]
-    same_sums = bool(np.array_equal(sums, check["sums"]))
-    return {"p": p, "trials": T, "gpu_counts": got, "cpu_counts": check["counts"],
-            "pd_gpu": got[0] / T, "pd_cpu": check["counts"][0] / T,
-            "sums_bit_exact_trials": ncal, "match": got == check["counts"] and same_sums}
+    big = {"m6": 131_072, "m2": 1_048_576, "r23_m4": 131_072}[config]
+    gb = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 1 << 40, (1 << 40) + big)["counts"].cpu().tolist()
+    n1, n2 = ntr, big
+
+    def ztest(x1, x2, t1, t2):
+        pool = (x1 + x2) / (t1 + t2)
+        sd = math.sqrt(max(pool * (1 - pool), 1e-12) * (1 / t1 + 1 / t2))
+        return abs(x1 / t1 - x2 / t2) / sd, 3.0 * sd
+
+    z_pd, tol_pd = ztest(c_cpu[0], gb[0], n1, n2)
+    z_pc, tol_pc = ztest(c_cpu[0] + c_cpu[1], gb[0] + gb[1], 2 * n1, 2 * n2)
+    exact = [int(x) for x in c_cpu] == got and bool(np.array_equal(sums, s_cpu))
+    pd_cpu, pd_gpu = c_cpu[0] / n1, gb[0] / n2
+    return {"point": {"N": N, "p": p, "learn_len": ll if ll else model.info()["learn_len_eff"],
+                      "model_rows": model.info()["n_rows"]},
+            "cpu": {"trials": n1, "counts": [int(x) for x in c_cpu], "Pd": pd_cpu,
+                    "Pc": (c_cpu[0] + c_cpu[1]) / (2 * n1), "seconds": t_cpu, "learn_s": t_cpu_learn,
+                    "threads": threads},
+            "gpu_same_trials": {"counts": got, "sums_bit_exact_trials": ncal, "learn_s": t_gpu_learn},
+            "gpu_large_sample": {"trials": n2, "first_trial": 1 << 40, "counts": gb, "Pd": pd_gpu,
+                                 "Pc": (gb[0] + gb[1]) / (2 * n2)},
+            "tolerance": "3 sigma of the difference of two binomial proportions (pooled)",
+            "pd_abs_diff": abs(pd_cpu - pd_gpu), "pd_tol": tol_pd, "pd_z": z_pd,
+            "pc_tol": tol_pc, "pc_z": z_pc,
+            "informative": 0.05 < pd_gpu < 0.95,
+            "exact_match": exact,
+            "match": exact and z_pd <= 3.0 and z_pc <= 3.0}
+
+
+def c0_demo(pkg, host):
+    """BASELINE.json configs[0], run in full: the demo preset (7,5) vs (5,7), m = 2,
+    N = 1e3, 1e3 trials over the demo's p grid -- the C oracle on this host (the CPU
+    path) and the product's run_experiment on the GPU; the Pd/Pc tables must be equal."""
+    from oracle import c_oracle as C
+    c = C0
+    threads = host["threads"]
+    c1, c2 = C.Code(c["gen1"], 2, 1, 2), C.Code(c["gen2"], 2, 1, 2)
+    rows_cpu = []
+    t0 = time.perf_counter()
+    for p in c["p_vec"]:
+        cnt, _ = C.Model(c1, p, None, 200, 1.0, c["seed"]).run_trials(c1, c2, c["N"], p, c["seed"], 0,
+                                                                       c["trials"], nthreads=threads)
+        rows_cpu.append({"N": c["N"], "p": p, "Pd": cnt[0] / c["trials"],
+                         "Pc": (int(cnt[0]) + int(cnt[1])) / (2 * c["trials"])})
+    t_cpu = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    df = pkg.run_experiment(1, 2, 2, c["gen1"], c["gen2"], c["trials"], c["p_vec"], None, 200, 1.0, c["seed"],
+                            N_list=[c["N"]])
+    t_gpu = time.perf_counter() - t0
+    rows_gpu = df.to_dict(orient="records")
+    return {"config": "demo preset (7,5) vs (5,7), m=2, N=1e3, 1e3 trials, p " + str(c["p_vec"]),
+            "cpu_seconds": t_cpu, "cpu_trials_per_s": len(c["p_vec"]) * c["trials"] / t_cpu, "cpu_threads": threads,
+            "gpu_seconds_incl_setup": t_gpu, "rows": rows_gpu, "match": rows_gpu == rows_cpu}
 
 
 if __name__ == "__main__":

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5
 
@@ -65,6 +65,16 @@ EXPORTS = {
     "cvd_model_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "cvd_model_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "cvd_model_destroy": (None, [ctypes.c_void_p]),
+    "cvd_model_save": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
+    "cvd_model_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "cvd_model_jit_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]),
+    "cvd_allreduce_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int32,
+                                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_void_p)]),
+    "cvd_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "cvd_comm_init": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.POINTER(ctypes.c_void_p)]),
+    "cvd_comm_allreduce_counts": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "cvd_comm_destroy": (None, [ctypes.c_void_p]),
     "cvd_generate": (ctypes.c_int, [ctypes.POINTER(cvd_code), ctypes.c_uint64, ctypes.c_uint32,
                                     ctypes.c_double, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,

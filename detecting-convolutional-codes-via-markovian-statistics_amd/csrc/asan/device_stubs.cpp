@@ -1,0 +1,13 @@
+// Host-only ASan/UBSan build of cvd_host.cpp (`make asan`): the device-side
+// entry points it calls are replaced by these stand-ins, so the BFS, the
+// learning chain, the P̂1 rows, the row tables and the model file I/O run under
+// the sanitizers without a GPU.  Test harness, not product code.
+#include "../cvd_internal.h"
+#include "../../../include/cvd.h"
+
+int cvd::upload_model(cvd_model&, int) {
+  cvd::set_error("no device in the host sanitizer build");
+  return CVD_E_UNSUPPORTED;
+}
+void cvd::free_model_device(cvd_model&) {}
+int cvd::explicit_kernel_of(const cvd_model& M) { return M.k1b_ok ? CVD_KERNEL_BUTTERFLY : CVD_KERNEL_NONE; }

@@ -28,6 +28,7 @@ using namespace cvd;
 
 static thread_local std::string g_err;
 void cvd::set_error(const std::string& msg) { g_err = msg; }
+std::string cvd::last_error_copy() { return g_err; }
 
 namespace {
 // CVD_SETUP_TIMING=1: phase times of cvd_model_create on stderr
@@ -742,6 +743,113 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
   CVD_CATCH
 }
 
+// ───────────────────────── ABI: on-disk model cache ──────────────────────────
+// A learned model is the reference's lru_cache entry (Pd_plotter.py:123-127) made
+// persistent: the learned rows (keys, log P̂1, successors, dense extras) are
+// written as length-prefixed blobs; the device-side tables (row hash, branch
+// metrics) are rebuilt from them at load, exactly as cvd_model_create does.
+
+namespace {
+constexpr char kMagic[4] = {'C', 'V', 'D', 'M'};
+constexpr uint32_t kFileVersion = 1;
+
+struct Writer {
+  FILE* f;
+  bool ok = true;
+  void raw(const void* p, size_t n) { ok = ok && std::fwrite(p, 1, n, f) == n; }
+  template <typename T>
+  void pod(const T& v) { raw(&v, sizeof(T)); }
+  template <typename T>
+  void vec(const std::vector<T>& v) {
+    const uint64_t n = v.size();
+    pod(n);
+    if (n) raw(v.data(), n * sizeof(T));
+  }
+};
+
+struct Reader {
+  FILE* f;
+  bool ok = true;
+  void raw(void* p, size_t n) { ok = ok && std::fread(p, 1, n, f) == n; }
+  template <typename T>
+  void pod(T& v) { raw(&v, sizeof(T)); }
+  template <typename T>
+  void vec(std::vector<T>& v, uint64_t max_elems = (uint64_t)1 << 34) {
+    uint64_t n = 0;
+    pod(n);
+    if (!ok || n > max_elems) { ok = false; return; }
+    v.resize((size_t)n);
+    if (n) raw(v.data(), (size_t)n * sizeof(T));
+  }
+};
+}  // namespace
+
+extern "C" int cvd_model_save(const cvd_model* Mo, const char* path) {
+  CVD_TRY
+  if (!Mo || !path) { set_error("null argument"); return CVD_E_INVALID; }
+  const std::string tmp = std::string(path) + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) { set_error(std::string("cannot write ") + tmp); return CVD_E_INVALID; }
+  Writer w{f};
+  w.raw(kMagic, 4);
+  w.pod(kFileVersion);
+  w.pod((int32_t)CVD_ABI_VERSION);
+  w.pod(Mo->dec);
+  w.pod(Mo->kind); w.pod(Mo->S); w.pod(Mo->learn_len_eff); w.pod(Mo->laplace); w.pod(Mo->logp1_unseen);
+  w.pod(Mo->n_rows);
+  w.vec(Mo->ltref); w.vec(Mo->keys); w.vec(Mo->logp1); w.vec(Mo->rec); w.vec(Mo->rowsum);
+  w.vec(Mo->p1_nz); w.vec(Mo->row_next);
+  const bool ok = w.ok && std::fclose(f) == 0;
+  if (!ok || std::rename(tmp.c_str(), path) != 0) {
+    std::remove(tmp.c_str());
+    set_error(std::string("cannot write ") + path);
+    return CVD_E_INVALID;
+  }
+  return CVD_OK;
+  CVD_CATCH
+}
+
+extern "C" int cvd_model_load(const char* path, cvd_model** out) {
+  CVD_TRY
+  if (!path || !out) { set_error("null argument"); return CVD_E_INVALID; }
+  *out = nullptr;
+  FILE* f = std::fopen(path, "rb");
+  if (!f) { set_error(std::string("cannot open ") + path); return CVD_E_INVALID; }
+  std::unique_ptr<FILE, int (*)(FILE*)> guard(f, std::fclose);
+  Reader r{f};
+  char magic[4];
+  uint32_t ver = 0;
+  int32_t abi = 0;
+  r.raw(magic, 4); r.pod(ver); r.pod(abi);
+  if (!r.ok || std::memcmp(magic, kMagic, 4) != 0 || ver != kFileVersion || abi != CVD_ABI_VERSION) {
+    set_error(std::string("not a model file of this build: ") + path);
+    return CVD_E_INVALID;
+  }
+  std::unique_ptr<cvd_model> Mo(new cvd_model());
+  r.pod(Mo->dec);
+  r.pod(Mo->kind); r.pod(Mo->S); r.pod(Mo->learn_len_eff); r.pod(Mo->laplace); r.pod(Mo->logp1_unseen);
+  r.pod(Mo->n_rows);
+  r.vec(Mo->ltref); r.vec(Mo->keys); r.vec(Mo->logp1); r.vec(Mo->rec); r.vec(Mo->rowsum);
+  r.vec(Mo->p1_nz); r.vec(Mo->row_next);
+  const CodeDesc& d = Mo->dec;
+  const bool shape_ok = d.k >= 1 && d.k <= kMaxK && d.n >= 1 && d.n <= kMaxN && d.m >= 1 && d.m <= kMaxM;
+  const size_t M = shape_ok ? (size_t)1 << d.m : 0, R = shape_ok ? (size_t)1 << d.n : 0;
+  if (!r.ok || !shape_ok || Mo->n_rows < 1 || Mo->keys.size() != (size_t)Mo->n_rows * M ||
+      Mo->logp1.size() != (size_t)Mo->n_rows * R || Mo->row_next.size() != (size_t)Mo->n_rows * R ||
+      Mo->ltref.size() != R + 1) {
+    set_error(std::string("corrupt model file: ") + path);
+    return CVD_E_INVALID;
+  }
+  if (explicit_supported(d.m, d.k, d.n)) {
+    Tabs T = make_tabs(Mo->dec);
+    build_hash(*Mo);
+    build_bmp(*Mo, T);
+  }
+  *out = Mo.release();
+  return CVD_OK;
+  CVD_CATCH
+}
+
 extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
   if (!Mo || !info) { set_error("null argument"); return CVD_E_INVALID; }
   info->kind = Mo->kind;
@@ -779,6 +887,17 @@ extern "C" int cvd_model_rows(const cvd_model* Mo, double* logp1_out, uint8_t* k
   if (logp1_out) std::memcpy(logp1_out, Mo->logp1.data(), (size_t)n_rows * R * sizeof(double));
   if (keys_out) std::memcpy(keys_out, Mo->keys.data(), (size_t)n_rows * M);
   return CVD_OK;
+}
+
+extern "C" int cvd_model_jit_status(const cvd_model* Mo, char* msg_out, int64_t msg_len) {
+  if (!Mo) { set_error("null model"); return CVD_E_INVALID; }
+  if (msg_out && msg_len > 0) {
+    const size_t n = std::min<size_t>(Mo->jit_error.size(), (size_t)msg_len - 1);
+    std::memcpy(msg_out, Mo->jit_error.data(), n);
+    msg_out[n] = 0;
+  }
+  if (Mo->device < 0 || !Mo->k1b_ok || Mo->hcap == 0) return 0;   // not applicable
+  return Mo->rtc_fn ? 1 : -1;
 }
 
 extern "C" int cvd_model_upload(cvd_model* Mo, int device) {

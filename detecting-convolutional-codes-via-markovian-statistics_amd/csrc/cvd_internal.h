@@ -50,6 +50,7 @@ struct cvd_model {
   uint32_t bfly_even[4] = {0, 0, 0, 0};   // nibble masks of the butterflies j with out(j, 0) in {00, 11}
   uint64_t bfly_x = 0;             // out(j, 0) in bits 2j..2j+1 (the specialisation key)
   void* rtc_fn = nullptr;          // hipFunction_t of the specialised kernel on `device`, if built
+  std::string jit_error;           // why the specialised kernel is unavailable (empty if built or n/a)
   std::vector<uint32_t> bfly;      // [2^m / 2]
 
   // device copies
@@ -68,6 +69,7 @@ struct cvd_model {
 namespace cvd {
 
 void set_error(const std::string& msg);
+std::string last_error_copy();
 inline int nib_words(int m) { return (1 << m) >= 8 ? (1 << m) / 8 : 1; }
 CVD_HD int row_words(int n) { return row_words_c(1 << n); }
 

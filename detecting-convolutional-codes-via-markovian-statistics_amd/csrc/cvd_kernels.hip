@@ -990,6 +990,13 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
 int cvd::upload_model(cvd_model& M, int device) {
   if (M.device == device) return CVD_OK;
   if (M.device >= 0) free_model_device(M);
+  // the caller's current device is restored on every return path
+  int cur = 0;
+  HIP_CHECK(hipGetDevice(&cur));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{cur};
   HIP_CHECK(hipSetDevice(device));
   int rc;
   if ((rc = dev_copy(M.d_ltref, M.ltref))) return rc;
@@ -1007,9 +1014,14 @@ int cvd::upload_model(cvd_model& M, int device) {
   }
   M.device = device;
   // code-specialised butterfly kernel (cvd_rtc.cpp); without it the compiled
-  // table-driven kernel runs
+  // table-driven kernel runs (same results), and the reason is kept for
+  // cvd_model_jit_status
   M.rtc_fn = nullptr;
-  if (M.k1b_ok && M.hcap > 0 && rtc_k1b_function(device, M.dec.m, M.bfly_x, &M.rtc_fn) != 0) M.rtc_fn = nullptr;
+  M.jit_error.clear();
+  if (M.k1b_ok && M.hcap > 0 && rtc_k1b_function(device, M.dec.m, M.bfly_x, &M.rtc_fn) != 0) {
+    M.rtc_fn = nullptr;
+    M.jit_error = last_error_copy();
+  }
   return CVD_OK;
 }
 

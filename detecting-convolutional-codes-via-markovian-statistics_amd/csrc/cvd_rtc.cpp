@@ -15,7 +15,13 @@
 // the comgr bundled with torch (an older LLVM), whose code for this kernel
 // spills and runs ~25% slower than the table-driven kernel -- so it is only
 // used when no clang is found.  If both fail, the launcher keeps the compiled
-// table-driven kernel (same results, slower).
+// table-driven kernel (same results, slower) and the model records why
+// (cvd_model_jit_status; the Python host warns).
+//
+// Code objects are cached on disk (CVD_JIT_CACHE, else $XDG_CACHE_HOME/cvd_jit,
+// else ~/.cache/cvd_jit; CVD_JIT_CACHE=off disables it), keyed by a hash of the
+// full kernel source, the target arch, the compiler path and flags, and the
+// tuning defines, so a later process with the same decoder skips the compile.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <fcntl.h>
@@ -44,6 +50,49 @@ namespace {
 
 std::mutex g_mu;
 std::map<std::tuple<int, int, uint64_t, std::string>, hipFunction_t> g_cache;
+
+uint64_t fnv1a(const std::string& s, uint64_t h = 0xcbf29ce484222325ull) {
+  for (unsigned char c : s) { h ^= c; h *= 0x100000001b3ull; }
+  return h;
+}
+
+std::string cache_dir() {
+  const char* e = std::getenv("CVD_JIT_CACHE");
+  if (e && std::string(e) == "off") return "";
+  std::string d;
+  if (e && e[0]) d = e;
+  else if (const char* x = std::getenv("XDG_CACHE_HOME")) d = std::string(x) + "/cvd_jit";
+  else if (const char* h = std::getenv("HOME")) d = std::string(h) + "/.cache/cvd_jit";
+  else return "";
+  // mkdir -p (the parent of a default path may not exist yet)
+  for (size_t i = 1; i <= d.size(); ++i)
+    if (i == d.size() || d[i] == '/') (void)::mkdir(d.substr(0, i).c_str(), 0755);
+  return d;
+}
+
+bool cache_load(const std::string& path, std::vector<char>& code) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  code.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+  return !code.empty();
+}
+
+void cache_store(const std::string& path, const std::vector<char>& code) {
+  const std::string tmp = path + ".tmp." + std::to_string(::getpid());
+  {
+    std::ofstream f(tmp, std::ios::binary);
+    if (!f) return;
+    f.write(code.data(), (std::streamsize)code.size());
+    if (!f) { ::unlink(tmp.c_str()); return; }
+  }
+  if (::rename(tmp.c_str(), path.c_str()) != 0) ::unlink(tmp.c_str());   // atomic publish
+}
+
+// flags of the clang compile (also part of the cache key)
+const char* kClangFlags[] = {"-O3", "-std=c++17", "-ffp-contract=off",
+                             // ILP-first machine scheduling: 1-2% faster per launch in the
+                             // interleaved A/B (profiles/r01g_ab/), same registers, no spills
+                             "-mllvm", "--amdgpu-sched-strategy=max-ilp"};
 
 std::string entry_source(int m, uint64_t xm) {
   char entry[256];
@@ -83,11 +132,9 @@ bool compile_clang(const std::string& src, const std::string& arch, std::vector<
     f << "#include <hip/hip_runtime.h>\n" << src;
   }
   const std::string arch_opt = "--offload-arch=" + arch;
-  std::vector<std::string> args = {clang, "-x", "hip", arch_opt, "--offload-device-only", "--no-gpu-bundle-output",
-                                   "-O3", "-std=c++17", "-ffp-contract=off",
-                                   // ILP-first machine scheduling: 1-2% faster per launch in the
-                                   // interleaved A/B (profiles/r01g_ab/), same registers, no spills
-                                   "-mllvm", "--amdgpu-sched-strategy=max-ilp", "-c", in, "-o", out};
+  std::vector<std::string> args = {clang, "-x", "hip", arch_opt, "--offload-device-only", "--no-gpu-bundle-output"};
+  for (const char* f : kClangFlags) args.push_back(f);
+  for (const char* f : {"-c", in.c_str(), "-o", out.c_str()}) args.push_back(f);
   if (const char* d = std::getenv("CVD_JIT_DEFINES")) {   // tuning experiments: -D and -mllvm <opt> only
     std::istringstream ds(d);
     std::string t, o;
@@ -179,19 +226,43 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out) {
   std::vector<char> code;
   std::string err1, err2;
   const char* via = std::getenv("CVD_JIT_VIA");   // "hiprtc" forces the fallback (tests)
-  const bool ok = (!(via && std::string(via) == "hiprtc") && compile_clang(src, arch, code, err1)) ||
-                  compile_hiprtc(src, arch, code, err2);
-  if (!ok) { set_error("JIT: " + err1 + " | " + err2); return -1; }
-
-  int cur = 0;
-  (void)hipGetDevice(&cur);
-  (void)hipSetDevice(device);
-  hipModule_t mod;
+  const bool force_rtc = via && std::string(via) == "hiprtc";
+  // on-disk cache of the clang-built code object
+  std::string cpath;
+  if (!force_rtc) {
+    const std::string dir = cache_dir();
+    std::string keytxt = src + "\n" + arch + "\n" + find_clang() + "\n" + (defs ? defs : "");
+    for (const char* f : kClangFlags) keytxt += std::string("\n") + f;
+    if (!dir.empty()) {
+      char name[64];
+      std::snprintf(name, sizeof(name), "/k1b_%016llx.co", (unsigned long long)fnv1a(keytxt));
+      cpath = dir + name;
+    }
+  }
+  auto load = [&](hipFunction_t& fn) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    hipModule_t mod;
+    const bool loaded = hipModuleLoadData(&mod, code.data()) == hipSuccess &&
+                        hipModuleGetFunction(&fn, mod, "cvd_k1b_spec") == hipSuccess;
+    (void)hipSetDevice(cur);
+    return loaded;
+  };
   hipFunction_t fn;
-  const bool loaded = hipModuleLoadData(&mod, code.data()) == hipSuccess &&
-                      hipModuleGetFunction(&fn, mod, "cvd_k1b_spec") == hipSuccess;
-  (void)hipSetDevice(cur);
-  if (!loaded) { set_error("JIT: module load failed"); return -1; }
+  if (!cpath.empty() && cache_load(cpath, code)) {
+    if (load(fn)) {
+      g_cache[key] = fn;
+      *fn_out = (void*)fn;
+      return 0;
+    }
+    ::unlink(cpath.c_str());   // unusable cached object: rebuild it
+  }
+  bool ok = !force_rtc && compile_clang(src, arch, code, err1);
+  if (ok && !cpath.empty()) cache_store(cpath, code);
+  if (!ok) ok = compile_hiprtc(src, arch, code, err2);
+  if (!ok) { set_error("JIT: " + err1 + " | " + err2); return -1; }
+  if (!load(fn)) { set_error("JIT: module load failed"); return -1; }
   g_cache[key] = fn;   // modules live for the process (one per device and code)
   *fn_out = (void*)fn;
   return 0;

@@ -15,7 +15,10 @@ cvd_generate (encoder + BSC into bit-packed HBM streams) and cvd_detect
 CPU fallback: without a GPU or without libcvd.so the calls raise.
 """
 import ctypes
+import hashlib
 import itertools
+import os
+import warnings
 from collections import OrderedDict
 
 import numpy as np
@@ -61,20 +64,68 @@ def _stream_ptr(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def model_cache_dir(explicit=None):
+    """Directory of the on-disk model cache: `explicit`, else $CVD_MODEL_CACHE; None
+    (no cache) when neither is set or the value is "off"."""
+    d = explicit if explicit is not None else os.environ.get("CVD_MODEL_CACHE")
+    if not d or d == "off":
+        return None
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def model_cache_key(dec, p, learn_len, learn_burn, laplace, seed, enum_cap, default_learn_len):
+    """File name of a learned model: a hash of everything the learning depends on,
+    the reference's lru_cache key (Pd_plotter.py:123-127: gens, k, n, m, p,
+    learn_len, learn_burn, laplace, seed) plus this build's enumeration policy and
+    stream spec."""
+    txt = repr((dec.key, float(p).hex(), learn_len, int(learn_burn), float(laplace).hex(), int(seed),
+                int(enum_cap), int(default_learn_len), _lib.ABI_VERSION, "philox4x32-10/D1-D4"))
+    return "cvdm_" + hashlib.sha256(txt.encode()).hexdigest()[:40] + ".bin"
+
+
 class Model:
     """Decoder trellis (G1) + learned P̂1 + T_ref(1/2) tables (a cvd_model)."""
 
     def __init__(self, dec, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345,
-                 enum_cap=DEFAULT_ENUM_CAP, default_learn_len=DEFAULT_SPARSE_LEARN_LEN):
+                 enum_cap=DEFAULT_ENUM_CAP, default_learn_len=DEFAULT_SPARSE_LEARN_LEN, cache_dir=None):
         self.dec = dec
         self.p = float(p)
+        self._lib = _lib.lib()
+        self.from_cache = False
+        path = None
+        d = model_cache_dir(cache_dir)
+        if d is not None:
+            path = os.path.join(d, model_cache_key(dec, p, learn_len, learn_burn, laplace, seed, enum_cap,
+                                                   default_learn_len))
+            if os.path.exists(path):
+                h = ctypes.c_void_p()
+                if self._lib.cvd_model_load(path.encode(), ctypes.byref(h)) == 0:
+                    self._h = h
+                    self.from_cache = True
+                    return
         prm = _lib.cvd_learn_params(float(p), -1 if learn_len is None else int(learn_len),
                                     int(learn_burn), float(laplace), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                     int(enum_cap), int(default_learn_len))
         h = ctypes.c_void_p()
-        _lib.check(_lib.lib().cvd_model_create(dec.c, ctypes.byref(prm), ctypes.byref(h)))
+        _lib.check(self._lib.cvd_model_create(dec.c, ctypes.byref(prm), ctypes.byref(h)))
         self._h = h
-        self._lib = _lib.lib()
+        if path is not None:
+            _lib.check(self._lib.cvd_model_save(self._h, path.encode()))
+
+    def save(self, path):
+        _lib.check(self._lib.cvd_model_save(self._h, os.fspath(path).encode()))
+
+    @classmethod
+    def load(cls, dec, path):
+        """A model written by save() (host tables; call upload(device) before use)."""
+        self = cls.__new__(cls)
+        self.dec, self._lib, self.from_cache = dec, _lib.lib(), True
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.cvd_model_load(os.fspath(path).encode(), ctypes.byref(h)))
+        self._h = h
+        self.p = float("nan")
+        return self
 
     @property
     def handle(self):
@@ -101,7 +152,17 @@ class Model:
 
     def upload(self, device):
         _lib.check(self._lib.cvd_model_upload(self._h, int(device)))
+        st, msg = self.jit_status()
+        if st < 0:
+            warnings.warn("code-specialised detector kernel unavailable, running the table-driven "
+                          f"butterfly kernel (same results, slower): {msg}", RuntimeWarning, stacklevel=2)
         return self
+
+    def jit_status(self):
+        """(1 built | -1 unavailable | 0 not applicable, reason) of the code-specialised kernel."""
+        buf = ctypes.create_string_buffer(4096)
+        st = self._lib.cvd_model_jit_status(self._h, buf, len(buf))
+        return st, buf.value.decode(errors="replace")
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -118,12 +179,13 @@ class Detector:
     like the reference's @lru_cache(maxsize=128) (Pd_plotter.py:123)."""
 
     def __init__(self, k, n, m, gen1, device=None, enum_cap=DEFAULT_ENUM_CAP,
-                 default_learn_len=DEFAULT_SPARSE_LEARN_LEN):
+                 default_learn_len=DEFAULT_SPARSE_LEARN_LEN, model_cache=None):
         self.k, self.n, self.m = int(k), int(n), int(m)
         self.dec = as_code(gen1, m, k, n)
         self.device = _require_gpu(device)
         self.enum_cap = enum_cap
         self.default_learn_len = default_learn_len
+        self.model_cache = model_cache   # on-disk cache dir (None: $CVD_MODEL_CACHE if set)
         self._models = OrderedDict()
 
     def model(self, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345):
@@ -132,7 +194,7 @@ class Detector:
             self._models.move_to_end(key)
             return self._models[key]
         mod = Model(self.dec, p, learn_len, learn_burn, laplace, seed, self.enum_cap,
-                    self.default_learn_len).upload(self.device.index)
+                    self.default_learn_len, self.model_cache).upload(self.device.index)
         self._models[key] = mod
         while len(self._models) > 128:
             self._models.popitem(last=False)
@@ -153,7 +215,8 @@ class Detector:
             nw = workers or min(len(keys), 8)
             with ThreadPoolExecutor(max_workers=nw) as ex:
                 built = list(ex.map(lambda p: Model(self.dec, p, learn_len, learn_burn, laplace, seed,
-                                                    self.enum_cap, self.default_learn_len), keys.values()))
+                                                    self.enum_cap, self.default_learn_len, self.model_cache),
+                                    keys.values()))
             for key, mod in zip(keys, built):
                 self._models[key] = mod.upload(self.device.index)
         return [self.model(p, learn_len, learn_burn, laplace, seed) for p in p_list]

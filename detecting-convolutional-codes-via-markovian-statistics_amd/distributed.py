@@ -27,7 +27,8 @@ def dist_info():
 
 def run_sharded(count_fn, N_list, p_vec, num_iter, device, rank=None, world=None):
     """counts[iN, ip, :] += count_fn(iN, N, ip, p, lo, hi, out) for this rank's
-    trial block, then one all_reduce.  `count_fn` accumulates (s1, s2) into the
+    trial block, then one all_reduce over the default process group (whenever one
+    is initialised, world 1 included).  `count_fn` accumulates (s1, s2) into the
     2-element tensor `out` (device-side for the GPU engine)."""
     import torch.distributed as tdist
     r0, w0 = dist_info()
@@ -38,9 +39,33 @@ def run_sharded(count_fn, N_list, p_vec, num_iter, device, rank=None, world=None
     for iN, N in enumerate(N_list):
         for ip, p in enumerate(p_vec):
             count_fn(iN, N, ip, p, lo, hi, counts[iN, ip])
-    if world > 1:
+    if tdist.is_available() and tdist.is_initialized():
         tdist.all_reduce(counts, op=tdist.ReduceOp.SUM)
     return counts
+
+
+def allreduce_counts(tensors, streams=None):
+    """SUM-reduce int64 count tensors, one per device of this process, in place
+    through the C-ABI's RCCL entry (cvd_allreduce_counts: ncclCommInitAll + one
+    grouped ncclAllReduce) -- the multi-GPU route for callers without
+    torch.distributed.  Synchronises the devices' streams before returning."""
+    import ctypes
+    from . import _lib
+    n = len(tensors)
+    if n == 0:
+        return tensors
+    length = tensors[0].numel()
+    for t in tensors:
+        if t.dtype != torch.int64 or not t.is_cuda or not t.is_contiguous() or t.numel() != length:
+            raise ValueError("allreduce_counts: contiguous int64 device tensors of one length")
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tensors])
+    devs = (ctypes.c_int32 * n)(*[t.device.index for t in tensors])
+    strm = (ctypes.c_void_p * n)(*[(s or torch.cuda.current_stream(t.device)).cuda_stream
+                                   for s, t in zip(streams or [None] * n, tensors)])
+    _lib.check(_lib.lib().cvd_allreduce_counts(ptrs, length, n, devs, strm))
+    for t in tensors:
+        torch.cuda.synchronize(t.device)
+    return tensors
 
 
 def pd_rows(counts, N_list, p_vec, num_iter):

@@ -13,7 +13,7 @@
  *                                                                                  cvd_generate (+ cvd_trace)
  *   Pd_plotter.py:106-116     log_prob_sequence                                    cvd_detect (per-sequence sums)
  *   Pd_plotter.py:198-233     trial loop, decision, Pd/Pc counting                 cvd_detect (counts) / cvd_mc_run
- *   (none: the reference is single-process)                                        counts reduced by the caller over RCCL
+ *   (none: the reference is single-process)                                        cvd_allreduce_counts / cvd_comm_* (RCCL)
  *   comp_parity.py:90-128     parity_satisfaction_fraction / parity_detector       cvd_parity_detect
  *                             (parity-template baseline)
  *   alpha_exponent.py:83-156  learn_transition_tensor (joint counts)              cvd_count_transitions
@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 3
+#define CVD_ABI_VERSION 4
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -116,7 +116,17 @@ int cvd_model_dense_P1(const cvd_model* model, double* P_out, int64_t S);
 /* Per-row tables (host copies): logP1[row*2^n + r]; keys[row][2^m] metric bytes. */
 int cvd_model_rows(const cvd_model* model, double* logp1_out, uint8_t* keys_out, int64_t n_rows);
 int cvd_model_upload(cvd_model* model, int device);
+/* The code-specialised detector kernel (CVD_KERNEL_BUTTERFLY_RTC) of an uploaded
+ * model: 1 = built, -1 = unavailable (msg_out receives the compiler's reason, the
+ * table-driven kernel runs instead with the same results), 0 = not applicable. */
+int cvd_model_jit_status(const cvd_model* model, char* msg_out, int64_t msg_len);
 void cvd_model_destroy(cvd_model* model);
+/* On-disk model cache (the reference memoises P̂1 per learning key with
+ * @lru_cache, Pd_plotter.py:123-127; this makes it persistent): save writes the
+ * learned rows atomically (tmp + rename); load rebuilds the model (host tables;
+ * upload it before use).  Files carry this build's ABI version. */
+int cvd_model_save(const cvd_model* model, const char* path);
+int cvd_model_load(const char* path, cvd_model** out);
 
 /* ---- device work ---------------------------------------------------------- */
 /* Encoder (enc) -> BSC(p) received words for sequences q0..q0+count-1 of an
@@ -157,6 +167,28 @@ int64_t cvd_mc_workspace_bytes(const cvd_code* enc1, int64_t N, int64_t batch);
 int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2,
                double p, int64_t N, uint64_t seed, int64_t trial_begin, int64_t trial_end,
                int64_t batch, void* d_work, int64_t* d_counts, int32_t path, void* stream);
+
+/* ---- multi-GPU: the one collective (none in the reference,
+ * Pd_plotter.py:176-235 is single-process) --------------------------------
+ * Sum-reduce the int64 success counts of a trial-sharded run over RCCL (xGMI).
+ * Shard the global trial range [0, num_iter) of every (N, p) grid point over the
+ * GPUs, run cvd_mc_run per shard into a per-device count buffer, reduce: every
+ * buffer then holds the single-process counts (streams are keyed by the global
+ * trial id).  Enqueued on the given streams (async; the caller synchronises).
+ *
+ * One process, ndev devices: d_counts[i] on devices[i], ordered after streams[i]
+ * (streams NULL or streams[i] NULL = that device's default stream).  The
+ * communicators are created on first use of a device list and cached. */
+int cvd_allreduce_counts(int64_t* const* d_counts, int64_t len, int32_t ndev, const int32_t* devices,
+                         void* const* streams);
+/* One process per GPU: rank 0 calls cvd_comm_unique_id and hands the 128 bytes to
+ * every rank (any channel); each rank calls cvd_comm_init with its device. */
+#define CVD_COMM_ID_BYTES 128
+typedef struct cvd_comm cvd_comm;
+int cvd_comm_unique_id(uint8_t* id_out /* [CVD_COMM_ID_BYTES] */);
+int cvd_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, cvd_comm** out);
+int cvd_comm_allreduce_counts(cvd_comm* comm, int64_t* d_counts, int64_t len, void* stream);
+void cvd_comm_destroy(cvd_comm* comm);
 
 /* ---- parity-template baseline (comp_parity.py, parity_eqn_check.py) --------
  * Per sequence q of a received-word buffer (pitch = nseq, layout as above):
