@@ -209,6 +209,8 @@ def main():
             ev[3].record(dstream)
 
     def run(steps, base, events=None):
+        if steps <= 0:
+            return
         if not a.overlap:
             for s in range(steps):
                 ev = events[s] if events else None

@@ -60,6 +60,9 @@ EXPORTS = {
                                      ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p, ctypes.c_void_p]),
     "cvd_model_create": (ctypes.c_int, [ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_learn_params),
                                         ctypes.POINTER(ctypes.c_void_p)]),
+    "cvd_model_create_device": (ctypes.c_int, [ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_learn_params),
+                                               ctypes.c_int32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                               ctypes.c_void_p]),
     "cvd_model_info_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cvd_model_info)]),
     "cvd_model_dense_P1": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "cvd_model_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),

@@ -594,7 +594,11 @@ bool cvd::explicit_supported(int m, int k, int n) {
   return shape && (L + 1) * n <= 15;
 }
 
-extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm, cvd_model** out) {
+namespace {
+// cvd_model_create / cvd_model_create_device: the learning chain on the host
+// (device < 0) or on a GPU (cvd_learn.hip; same outputs), everything else shared.
+int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, void* stream, cvd_model** out,
+                 LearnStats* stats) {
   CVD_TRY
   if (!prm || !out) { set_error("null argument"); return CVD_E_INVALID; }
   *out = nullptr;
@@ -643,13 +647,19 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
     const int64_t L = prm->learn_len < 0 ? std::max<int64_t>(5000, 200 * S) : prm->learn_len;
     Mo->learn_len_eff = L;
     std::vector<int64_t> cnt((size_t)S * R, 0);
-    HostStream hs(Mo->dec, T, seed, kLearnTag, 0, prm->p, true);
-    int64_t i = 0;   // D_0 = 0 is BFS index 0
-    for (int64_t t = 0; t < L; ++t) {
-      const uint32_t r = hs.next_word(t);
-      if (t >= prm->learn_burn) cnt[(size_t)i * R + r]++;
-      i = next[(size_t)i * R + r];
+    if (device >= 0) {
+      rc = device_learn_dense(Mo->dec, next, S, L, prm->learn_burn, seed, prm->p, device, stream, cnt, stats);
+      if (rc) return rc;
+    } else {
+      HostStream hs(Mo->dec, T, seed, kLearnTag, 0, prm->p, true);
+      int64_t i = 0;   // D_0 = 0 is BFS index 0
+      for (int64_t t = 0; t < L; ++t) {
+        const uint32_t r = hs.next_word(t);
+        if (t >= prm->learn_burn) cnt[(size_t)i * R + r]++;
+        i = next[(size_t)i * R + r];
+      }
     }
+    pt.mark("chain");
     Mo->n_rows = S;
     Mo->keys = std::move(states);
     Mo->logp1.assign((size_t)S * R, 0.0);
@@ -688,24 +698,40 @@ extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm
     Mo->learn_len_eff = L;
     std::vector<uint8_t> keys;
     StateMap map(M, &keys);
-    map.reserve(std::min<int64_t>(L + 1, (int64_t)1 << 26));
     std::vector<int64_t> cnt;
-    std::vector<uint8_t> D((size_t)M, 0), Dn((size_t)M);
-    const HostStep step(T);
-    bool ins;
-    int64_t i = map.insert(D.data(), ins);
-    cnt.resize((size_t)R, 0);
-    HostStream hs(Mo->dec, T, seed, kLearnTag, 0, prm->p, true);
-    for (int64_t t = 0; t < L; ++t) {
-      const uint32_t r = hs.next_word(t);
-      if (t >= prm->learn_burn) cnt[(size_t)i * R + r]++;
-      step(D.data(), r, Dn.data());
-      int64_t j = map.insert(Dn.data(), ins);
-      if (ins) cnt.resize((size_t)map.count * R, 0);
-      std::swap(D, Dn);
-      i = j;
+    if (device >= 0) {
+      // the chain on the GPU: rows in first-visit order + counts; the host map is
+      // rebuilt from the rows (insertion order = row order) for the successors
+      std::vector<uint8_t> rows;
+      int64_t Sd = 0;
+      rc = device_learn_sparse(Mo->dec, L, prm->learn_burn, seed, prm->p, device, stream, rows, cnt, Sd, stats);
+      if (rc) return rc;
+      map.reserve(Sd);
+      bool ins;
+      for (int64_t s = 0; s < Sd; ++s) {
+        map.insert(rows.data() + (size_t)s * M, ins);
+        if (!ins) { set_error("GPU learning: duplicate row key"); return CVD_E_STATE; }
+      }
+    } else {
+      map.reserve(std::min<int64_t>(L + 1, (int64_t)1 << 26));
+      std::vector<uint8_t> D((size_t)M, 0), Dn((size_t)M);
+      const HostStep step(T);
+      bool ins;
+      int64_t i = map.insert(D.data(), ins);
+      cnt.resize((size_t)R, 0);
+      HostStream hs(Mo->dec, T, seed, kLearnTag, 0, prm->p, true);
+      for (int64_t t = 0; t < L; ++t) {
+        const uint32_t r = hs.next_word(t);
+        if (t >= prm->learn_burn) cnt[(size_t)i * R + r]++;
+        step(D.data(), r, Dn.data());
+        int64_t j = map.insert(Dn.data(), ins);
+        if (ins) cnt.resize((size_t)map.count * R, 0);
+        std::swap(D, Dn);
+        i = j;
+      }
     }
     pt.mark("chain");
+    const HostStep step(T);
     S = map.count;
     Mo->S = S;
     Mo->n_rows = S;
@@ -848,6 +874,28 @@ extern "C" int cvd_model_load(const char* path, cvd_model** out) {
   *out = Mo.release();
   return CVD_OK;
   CVD_CATCH
+}
+}  // namespace
+
+extern "C" int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm, cvd_model** out) {
+  return model_create(dec, prm, -1, nullptr, out, nullptr);
+}
+
+extern "C" int cvd_model_create_device(const cvd_code* dec, const cvd_learn_params* prm, int32_t device,
+                                       void* stream, cvd_model** out, double* stats_out) {
+  if (device < 0) { set_error("device must be >= 0"); return CVD_E_INVALID; }
+  LearnStats st;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = model_create(dec, prm, device, stream, out, &st);
+  st.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (stats_out) {
+    stats_out[0] = st.seconds;
+    stats_out[1] = (double)st.mismatched_blocks;
+    stats_out[2] = (double)st.fix_passes;
+    stats_out[3] = (double)st.sequential_blocks;
+    stats_out[4] = (double)st.hash_attempts;
+  }
+  return rc;
 }
 
 extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {

@@ -97,4 +97,22 @@ int rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);
 
+// P̂1 learning chain on the GPU (cvd_learn.hip): identical outputs to the host chain.
+struct LearnStats {
+  int64_t mismatched_blocks = 0;   // speculative blocks whose start failed verification
+  int64_t fix_passes = 0;          // re-run passes
+  int64_t sequential_blocks = 0;   // blocks re-run one by one (cascading mismatches)
+  int64_t hash_attempts = 0;       // sort passes (>1: a 64-bit key-hash collision was seen)
+  double seconds = 0.0;
+};
+// sparse model: rows = distinct D_0..D_L in first-visit order (keys_out [S][2^m]
+// bytes), cnt_out[S][2^n] = transitions over t in [burn, L)
+int device_learn_sparse(const CodeDesc& dec, int64_t L, int64_t burn, uint64_t seed, double p, int device,
+                        void* stream, std::vector<uint8_t>& keys_out, std::vector<int64_t>& cnt_out,
+                        int64_t& S_out, LearnStats* stats);
+// dense model: the chain on the BFS automaton next[S][2^n] from index 0
+int device_learn_dense(const CodeDesc& dec, const std::vector<int32_t>& next, int64_t S, int64_t L, int64_t burn,
+                       uint64_t seed, double p, int device, void* stream, std::vector<int64_t>& cnt_out,
+                       LearnStats* stats);
+
 }  // namespace cvd

@@ -88,11 +88,15 @@ class Model:
     """Decoder trellis (G1) + learned P̂1 + T_ref(1/2) tables (a cvd_model)."""
 
     def __init__(self, dec, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345,
-                 enum_cap=DEFAULT_ENUM_CAP, default_learn_len=DEFAULT_SPARSE_LEARN_LEN, cache_dir=None):
+                 enum_cap=DEFAULT_ENUM_CAP, default_learn_len=DEFAULT_SPARSE_LEARN_LEN, cache_dir=None,
+                 learn_device=None):
+        """learn_device: run the learning chain on this GPU (cvd_model_create_device,
+        bit-identical to the host chain); None: on the host (cvd_model_create)."""
         self.dec = dec
         self.p = float(p)
         self._lib = _lib.lib()
         self.from_cache = False
+        self.learn_stats = None
         path = None
         d = model_cache_dir(cache_dir)
         if d is not None:
@@ -108,7 +112,14 @@ class Model:
                                     int(learn_burn), float(laplace), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                     int(enum_cap), int(default_learn_len))
         h = ctypes.c_void_p()
-        _lib.check(self._lib.cvd_model_create(dec.c, ctypes.byref(prm), ctypes.byref(h)))
+        if learn_device is None:
+            _lib.check(self._lib.cvd_model_create(dec.c, ctypes.byref(prm), ctypes.byref(h)))
+        else:
+            st = (ctypes.c_double * 5)()
+            _lib.check(self._lib.cvd_model_create_device(dec.c, ctypes.byref(prm), int(learn_device), None,
+                                                         ctypes.byref(h), ctypes.cast(st, ctypes.c_void_p)))
+            self.learn_stats = dict(zip(("seconds", "mismatched_blocks", "fix_passes", "sequential_blocks",
+                                         "hash_attempts"), list(st)))
         self._h = h
         if path is not None:
             _lib.check(self._lib.cvd_model_save(self._h, path.encode()))
@@ -186,6 +197,9 @@ class Detector:
         self.enum_cap = enum_cap
         self.default_learn_len = default_learn_len
         self.model_cache = model_cache   # on-disk cache dir (None: $CVD_MODEL_CACHE if set)
+        # the learning chain runs on this GPU (bit-identical to the host chain);
+        # CVD_LEARN_HOST=1 keeps it on the host
+        self.learn_device = None if os.environ.get("CVD_LEARN_HOST", "0") not in ("", "0") else self.device.index
         self._models = OrderedDict()
 
     def model(self, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345):
@@ -194,7 +208,7 @@ class Detector:
             self._models.move_to_end(key)
             return self._models[key]
         mod = Model(self.dec, p, learn_len, learn_burn, laplace, seed, self.enum_cap,
-                    self.default_learn_len, self.model_cache).upload(self.device.index)
+                    self.default_learn_len, self.model_cache, self.learn_device).upload(self.device.index)
         self._models[key] = mod
         while len(self._models) > 128:
             self._models.popitem(last=False)
@@ -215,7 +229,8 @@ class Detector:
             nw = workers or min(len(keys), 8)
             with ThreadPoolExecutor(max_workers=nw) as ex:
                 built = list(ex.map(lambda p: Model(self.dec, p, learn_len, learn_burn, laplace, seed,
-                                                    self.enum_cap, self.default_learn_len, self.model_cache),
+                                                    self.enum_cap, self.default_learn_len, self.model_cache,
+                                                    self.learn_device),
                                     keys.values()))
             for key, mod in zip(keys, built):
                 self._models[key] = mod.upload(self.device.index)

@@ -8,7 +8,8 @@
  *   viterbi_markov.py:139-159 viterbi_metric_step (Eq. 4-5)                        cvd_metric_step (host), cvd_trace (GPU)
  *   viterbi_markov.py:166-195 enumerate_markov_states_allzero (BFS)                cvd_enumerate
  *   viterbi_markov.py:202-230 + Pd_plotter.py:89-99  T(p) at p = 1/2              cvd_model_* (|Y(i,j)|/2^n, exact)
- *   Pd_plotter.py:123-169     learn_P1_empirical                                   cvd_model_create
+ *   Pd_plotter.py:123-169     learn_P1_empirical                                   cvd_model_create (host chain),
+ *                                                                                  cvd_model_create_device (GPU chain)
  *   viterbi_markov.simulate_markov_sequence (MISSING; called Pd_plotter.py:149,212,219)
  *                                                                                  cvd_generate (+ cvd_trace)
  *   Pd_plotter.py:106-116     log_prob_sequence                                    cvd_detect (per-sequence sums)
@@ -110,6 +111,14 @@ int cvd_enumerate(const cvd_code* dec, int64_t cap, int64_t* S_out,
 
 /* ---- model: decoder trellis + learned P̂1 + T_ref(1/2) ------------------------ */
 int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm, cvd_model** out);
+/* The same model with the learning chain (Pd_plotter.py:143-163) run on GPU `device`
+ * (parallel in time: speculative blocks verified at their boundaries, first visits
+ * by a radix sort of key hashes; see cvd_learn.hip).  Bit-identical to
+ * cvd_model_create.  stats_out (nullable) [5]: seconds, mismatched speculative
+ * blocks, re-run passes, blocks re-run sequentially, hash/sort attempts.
+ * Synchronous; `stream` orders the device work (NULL = default stream). */
+int cvd_model_create_device(const cvd_code* dec, const cvd_learn_params* prm, int32_t device, void* stream,
+                            cvd_model** out, double* stats_out);
 int cvd_model_info_get(const cvd_model* model, cvd_model_info* info);
 /* Dense models: the S x S P̂1 matrix exactly as Pd_plotter.py:166-167 builds it. */
 int cvd_model_dense_P1(const cvd_model* model, double* P_out, int64_t S);

@@ -90,9 +90,11 @@ def test_bench_launches_its_own_ranks(tmp_path):
     common = ["--config", "m2", "--N", "1000", "--batch", "65536", "--warmup", "0", "--p", "0.092",
               "--cpu-baseline", "0"]
     two = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-                          "--steps", "2", *common], check=True, timeout=300, capture_output=True, text=True, env=env)
+                          "--steps", "2", *common], timeout=300, capture_output=True, text=True, env=env)
+    assert two.returncode == 0, two.stderr[-4000:]
     one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "4", *common],
-                         check=True, timeout=300, capture_output=True, text=True, env=env)
+                         timeout=300, capture_output=True, text=True, env=env)
+    assert one.returncode == 0, one.stderr[-4000:]
     j2 = json.loads([ln for ln in two.stdout.splitlines() if ln.startswith("{")][-1])
     j1 = json.loads([ln for ln in one.stdout.splitlines() if ln.startswith("{")][-1])
     assert j2["n_gpus"] == 2 and j1["n_gpus"] == 1
