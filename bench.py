@@ -56,6 +56,12 @@ PD_POINTS = {
     "m2": {"N": 10_000, "p": 0.092, "learn_len": None},             # Pd ~ 0.57
     "r23_m4": {"N": 100_000, "p": 0.0135, "learn_len": None},       # Pd ~ 0.33
 }
+# The points were chosen on the first trial ids (0..2000) of seed 12345, so the check runs
+# on fresh ids: the CPU sample (and the GPU's exact repeat of it) starts at trial 10^6, the
+# large GPU sample at 2^40.  (Selection and confirmation data kept apart: the first ~800
+# trials of seed 12345 at the m6 point are a 3-4 sigma low outlier -- profiles/diag/ shows
+# it follows those streams, not the model, and that seeds 1-7 and 99 show no such deficit.)
+PD_SAMPLE_START = 1_000_000
 # C0: demo_script.py preset 1 as BASELINE.json configs[0] states it -- (7,5) vs (5,7),
 # m = 2, N = 1e3, 1e3 trials, the demo's p grid and seed (demo_script.py:114-131)
 C0 = {"gen1": [[[1, 1, 1]], [[1, 0, 1]]], "gen2": [[[1, 0, 1]], [[1, 1, 1]]], "N": 1000, "trials": 1000,
@@ -336,9 +342,16 @@ def main():
         out["cpu_baseline"], _ = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds, host)
         out["pd_match_vs_cpu"] = pd_match(pkg, det, cc, a.config, k, n, m, a.seed, a.cpu_seconds, host)
         out["c0_demo"] = c0_demo(pkg, host)
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out, default=_json_default), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def _json_default(o):
+    """numpy scalars (counts, flags) in the output line"""
+    if hasattr(o, "item"):
+        return o.item()
+    raise TypeError(f"not JSON serializable: {type(o).__name__}")
 
 
 def host_info(threads=None):
@@ -414,19 +427,21 @@ def pd_match(pkg, det, cc, config, k, n, m, seed, seconds, host):
     c1, c2 = C.Code(cc["gen1"], m, k, n), C.Code(cc["gen2"], m, k, n)
     cm = C.Model(c1, p, ll, 200, 1.0, seed)
     t_cpu_learn = time.perf_counter() - t0
-    ntr = _sized_sample(lambda lo, hi: cm.run_trials(c1, c2, N, p, seed, lo, hi, nthreads=threads),
+    a0 = PD_SAMPLE_START
+    ntr = _sized_sample(lambda lo, hi: cm.run_trials(c1, c2, N, p, seed, a0 + lo, a0 + hi, nthreads=threads),
                         threads, seconds, threads)
     ntr = max(ntr, 64)
     t0 = time.perf_counter()
-    c_cpu, _ = cm.run_trials(c1, c2, N, p, seed, 0, ntr, nthreads=threads)
+    c_cpu, _ = cm.run_trials(c1, c2, N, p, seed, a0, a0 + ntr, nthreads=threads)
+    c_cpu = [int(x) for x in c_cpu]
     t_cpu = time.perf_counter() - t0
     ncal = min(16, ntr)
-    _, s_cpu = cm.run_trials(c1, c2, N, p, seed, 0, ncal, sums=True, nthreads=threads)
+    _, s_cpu = cm.run_trials(c1, c2, N, p, seed, a0, a0 + ncal, sums=True, nthreads=threads)
     t0 = time.perf_counter()
     model = det.model(p, ll, 200, 1.0, seed)
     t_gpu_learn = time.perf_counter() - t0
-    got = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 0, ntr)["counts"].cpu().tolist()
-    sums = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 0, ncal, return_sums=True)["sums"]
+    got = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, a0, a0 + ntr)["counts"].cpu().tolist()
+    sums = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, a0, a0 + ncal, return_sums=True)["sums"]
     big = {"m6": 131_072, "m2": 1_048_576, "r23_m4": 131_072}[config]
     gb = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, seed, 1 << 40, (1 << 40) + big)["counts"].cpu().tolist()
     n1, n2 = ntr, big
@@ -442,7 +457,7 @@ def pd_match(pkg, det, cc, config, k, n, m, seed, seconds, host):
     pd_cpu, pd_gpu = c_cpu[0] / n1, gb[0] / n2
     return {"point": {"N": N, "p": p, "learn_len": ll if ll else model.info()["learn_len_eff"],
                       "model_rows": model.info()["n_rows"]},
-            "cpu": {"trials": n1, "counts": [int(x) for x in c_cpu], "Pd": pd_cpu,
+            "cpu": {"trials": n1, "first_trial": a0, "counts": [int(x) for x in c_cpu], "Pd": pd_cpu,
                     "Pc": (c_cpu[0] + c_cpu[1]) / (2 * n1), "seconds": t_cpu, "learn_s": t_cpu_learn,
                     "threads": threads},
             "gpu_same_trials": {"counts": got, "sums_bit_exact_trials": ncal, "learn_s": t_gpu_learn},
@@ -451,9 +466,9 @@ def pd_match(pkg, det, cc, config, k, n, m, seed, seconds, host):
             "tolerance": "3 sigma of the difference of two binomial proportions (pooled)",
             "pd_abs_diff": abs(pd_cpu - pd_gpu), "pd_tol": tol_pd, "pd_z": z_pd,
             "pc_tol": tol_pc, "pc_z": z_pc,
-            "informative": 0.05 < pd_gpu < 0.95,
-            "exact_match": exact,
-            "match": exact and z_pd <= 3.0 and z_pc <= 3.0}
+            "informative": bool(0.05 < pd_gpu < 0.95),
+            "exact_match": bool(exact),
+            "match": bool(exact and z_pd <= 3.0 and z_pc <= 3.0)}
 
 
 def c0_demo(pkg, host):
@@ -469,7 +484,7 @@ def c0_demo(pkg, host):
     for p in c["p_vec"]:
         cnt, _ = C.Model(c1, p, None, 200, 1.0, c["seed"]).run_trials(c1, c2, c["N"], p, c["seed"], 0,
                                                                        c["trials"], nthreads=threads)
-        rows_cpu.append({"N": c["N"], "p": p, "Pd": cnt[0] / c["trials"],
+        rows_cpu.append({"N": c["N"], "p": p, "Pd": int(cnt[0]) / c["trials"],
                          "Pc": (int(cnt[0]) + int(cnt[1])) / (2 * c["trials"])})
     t_cpu = time.perf_counter() - t0
     t0 = time.perf_counter()
@@ -479,7 +494,7 @@ def c0_demo(pkg, host):
     rows_gpu = df.to_dict(orient="records")
     return {"config": "demo preset (7,5) vs (5,7), m=2, N=1e3, 1e3 trials, p " + str(c["p_vec"]),
             "cpu_seconds": t_cpu, "cpu_trials_per_s": len(c["p_vec"]) * c["trials"] / t_cpu, "cpu_threads": threads,
-            "gpu_seconds_incl_setup": t_gpu, "rows": rows_gpu, "match": rows_gpu == rows_cpu}
+            "gpu_seconds_incl_setup": t_gpu, "rows": rows_gpu, "match": bool(rows_gpu == rows_cpu)}
 
 
 if __name__ == "__main__":
