@@ -96,6 +96,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="C oracle threads (default: the host CPUs this process may run on, capped by "
                          "OMP_NUM_THREADS when set -- the GPU box's CPU share)")
+    ap.add_argument("--early-decision", type=int, default=1,
+                    help="also time the same steps with early decision (counts only; a trial stops once "
+                         "its decision is certain) and check its counts equal the full run's -- reported "
+                         "beside the headline, which always runs every step of every trial")
     ap.add_argument("--pmc-traffic", default=None,
                     help="per-launch detector counter summary of rocprofv3 --pmc passes "
                          "(profiles/collect.sh + summarize.py; default profiles/pmc_<detector>_<config>.json); "
@@ -202,6 +206,8 @@ def main():
         if ev is not None:
             ev[1].record(gstream)
 
+    early = [False]
+
     def detect(s, ev=None):
         p = p_grid[s % len(p_grid)]
         if ev is not None:
@@ -210,7 +216,8 @@ def main():
             pkg.parity_detect(bufs[s % nbuf], n, N, 2 * B, B, tpl, a.gamma, counts=counts[s % len(p_grid)],
                               stream=dstream)
         else:
-            det.detect(models[p], bufs[s % nbuf], N, 2 * B, B, counts=counts[s % len(p_grid)], stream=dstream)
+            det.detect(models[p], bufs[s % nbuf], N, 2 * B, B, counts=counts[s % len(p_grid)], stream=dstream,
+                       early_decision=early[0])
         if ev is not None:
             ev[3].record(dstream)
 
@@ -264,6 +271,39 @@ def main():
     gen_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     det_each = [e[2].elapsed_time(e[3]) for e in events]
     det_ms = float(np.mean(det_each))
+
+    # the same steps (same trial ids) with early decision: counts must be identical
+    early_out = None
+    if a.early_decision and not parity:
+        full_counts = counts.clone()
+        counts.zero_()
+        early[0] = True
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        ev2 = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(a.steps)]
+        t1 = time.perf_counter()
+        run(a.steps, 0, ev2)
+        if dist:
+            dist.all_reduce(counts)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t1
+        if dist:
+            t = torch.tensor([el2], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+        early[0] = False
+        d2 = [e[2].elapsed_time(e[3]) for e in ev2]
+        early_out = {"value": a.steps * B * world / el2, "unit": "trials/s", "ms_per_step": el2 / a.steps * 1e3,
+                     "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): d2[s] for s in range(a.steps)},
+                     "counts_equal_full_run": bool(torch.equal(counts, full_counts)),
+                     "note": "counts only: each trial stops once its decision is certain (rigorous IEEE "
+                             "bounds on the remaining increments, CVD_DETECT_EARLY_DECISION); the "
+                             "headline value above runs every step of every trial"}
+        counts.copy_(full_counts)
 
     if rank != 0:
         if dist:
@@ -337,6 +377,8 @@ def main():
                        "detector_ms_steps": det_each,
                        "per_p": per_p},
     }
+    if early_out is not None:
+        out["early_decision"] = early_out
     if a.cpu_baseline and world == 1 and not parity:
         host = host_info(a.cpu_threads)
         out["cpu_baseline"], _ = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds, host)

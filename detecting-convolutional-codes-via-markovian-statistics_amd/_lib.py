@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
 ABI_VERSION = 4
 
 PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5
+DETECT_EARLY_DECISION = 0x100   # OR'ed into path: counts only, stop once every decision is certain
 
 
 class CvdError(RuntimeError):

@@ -101,6 +101,37 @@ __device__ __forceinline__ void count_decisions(bool valid, bool is_h1, double l
   }
 }
 
+// ───────────────────────── early decision (counts only) ──────────────────────
+//
+// A trial's decision compares only the FINAL sums (Pd_plotter.py:215, :222:
+// success iff logP1 > logTref for H1, logP1 <= logTref for H2).  Every log P̂1
+// increment is <= 0 and at least lp_min; every log T_ref increment is <= 0 and
+// at least lt_min = log(1/2^n) (the observed word always counts, c >= 1).  With
+// rem steps left, in IEEE double with round-to-nearest (u = 2^-53):
+//   lp_final <= lp                              (adding a <= 0 never rounds up)
+//   lr_final >= (lr + rem * lt_min) (1 + u)^rem  (each rounding enlarges a negative
+//                                                 partial sum by at most a factor 1 + u)
+// and symmetrically lr_final <= lr, lp_final >= (lp + rem * lp_min)(1 + u)^rem.
+// The bounds below use the factor 1 + (4 rem + 32) u, which also covers the
+// rounding of the bound's own three operations.  So
+//   lp <= (lr + rem lt_min) f   =>  lp_final <= lr_final   (returns 1)
+//   (lp + rem lp_min) f > lr    =>  lp_final >  lr_final   (returns 2)
+// and the decision is certain from there on: the lane's count is exactly what the
+// full recursion gives.  Used only when per-trial sums are not requested; a wave
+// stops when every lane has decided.
+__device__ __forceinline__ int early_decide(double lp, double lr, int64_t rem, double lt_min, double lp_min) {
+  const double f = 1.0 + (double)(4 * rem + 32) * 0x1p-53;
+  if (lp <= (lr + (double)rem * lt_min) * f) return 1;
+  if ((lp + (double)rem * lp_min) * f > lr) return 2;
+  return 0;
+}
+// (lp, lr) stand-ins with the decided comparison for count_decisions
+__device__ __forceinline__ void early_final(int dec, double& lp, double& lr) {
+  if (dec == 1) { lp = -1.0; lr = 0.0; }
+  if (dec == 2) { lp = 1.0; lr = 0.0; }
+}
+constexpr int kEarlyEvery = 128;   // steps between checks (the k = 1 butterfly renormalisation period)
+
 // ────────────────────────── explicit metric path ────────────────────────────
 
 struct ExpArgs {
@@ -121,6 +152,8 @@ struct ExpArgs {
   double* sums;
   int64_t* counts;
   uint8_t* trace;
+  int32_t early;            // early decision (counts only; sums == nullptr)
+  double lt_min, lp_min;    // smallest log T_ref / log P̂1 increments (early_decide)
 };
 
 // Received words of one sequence, one word of lookahead (the next step's r is
@@ -548,6 +581,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     // needs the next word
     int64_t t = 0;
     int g = 0;
+    int dec = 0;   // early decision of this lane (0 = open)
     for (; t + 4 <= N; t += 4) {
       const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(nw, cw, 24);
       step(bits2(win, 0), bits2(win, 2), t + 1, IntC<1>{});
@@ -566,6 +600,14 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
         for (int i = 0; i < H; ++i) Dp[i] = as_u32(as_us2(Dp[i]) - o2);
         O = 0u;
         O8 = 0u;
+        static_assert(kRenorm == kEarlyEvery, "early checks ride on the renormalisation");
+        if (a.early) {
+          if (!dec) dec = early_decide(lp, lr, N - (t + 4), a.lt_min, a.lp_min);
+          if (__ballot(dec == 0) == 0) {   // every lane decided: the wave is done
+            t = N;
+            break;
+          }
+        }
       }
     }
     // last 1-3 steps (inside the current group, so no renormalisation is due)
@@ -580,6 +622,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       a.sums[2 * qe] = lp;
       a.sums[2 * qe + 1] = lr;
     }
+    early_final(dec, lp, lr);
   }
   count_decisions_masked(vmask, hmask, lp, lr, a.counts);
 }

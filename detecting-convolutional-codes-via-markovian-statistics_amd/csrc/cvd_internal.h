@@ -16,6 +16,7 @@ struct cvd_model {
   int64_t learn_len_eff = 0;
   double laplace = 1.0;
   double logp1_unseen = 0.0;  // log P̂1 of an unvisited row: log(λ / (S λ))
+  double lp_min = 0.0;        // smallest log P̂1 a step can add (early decision bound; set at upload)
   std::vector<double> ltref;  // ltref[c] = log(max(c / 2^n, 1e-300)), c = 0..2^n
 
   // rows (dense: BFS order; sparse: first-visit order of the learning chain)
@@ -81,10 +82,10 @@ int launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag,
                     int64_t N, int random_input, int64_t seq_base, int64_t seq_stride,
                     uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream);
 int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
-                        int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream);
+                        int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream, bool early = false);
 int launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                            int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
-                           void* stream, int variant);
+                           void* stream, int variant, bool early = false);
 // launch_detect_explicit variants
 constexpr int kExplicitBest = 0, kExplicitOrbit = 1, kExplicitGeneric = 2, kExplicitButterfly = 3;
 int upload_model(cvd_model& M, int device);

@@ -349,6 +349,8 @@ struct TabArgs {
   const uint32_t* r;
   double* sums;
   int64_t* counts;
+  int32_t early;            // early decision (counts only; sums == nullptr), see early_decide
+  double lt_min, lp_min;
 };
 
 template <bool kLds>
@@ -377,7 +379,12 @@ __global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
     const int64_t nwords = (a.N + spw - 1) / spw;
     uint32_t st = 0;                     // index of D_0 = 0 (first BFS state)
     uint4 cache;
+    int dec = 0;                         // early decision (0 = open)
     for (int64_t w = 0; w < nwords; ++w) {
+      if (a.early && w > 0 && (w & 7) == 0) {   // every 8 words
+        if (!dec) dec = early_decide(lp, lr, a.N - w * spw, a.lt_min, a.lp_min);
+        if (__ballot(dec == 0) == 0) break;
+      }
       uint32_t word = next_word(a.r, a.nseq, q, w, cache);
       const int ns = (int)min((int64_t)spw, a.N - w * spw);
       for (int i = 0; i < ns; ++i) {
@@ -390,6 +397,7 @@ __global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
       }
     }
     if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+    early_final(dec, lp, lr);
   }
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
@@ -440,7 +448,12 @@ __global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
     if (nchunks > 0) cur = rc[0];
     if (nchunks > 1) nxt = rc[cs];
     uint32_t st = 0;                              // index of D_0 = 0 (first BFS state)
+    int dec = 0;                                  // early decision (0 = open)
     for (int64_t c = 0; c < nchunks; ++c) {
+      if (a.early && c > 0 && (c & 1) == 0 && c <= full) {   // every 2 chunks (8 words)
+        if (!dec) dec = early_decide(lp, lr, N - c * 4 * SPW, a.lt_min, a.lp_min);
+        if (__ballot(dec == 0) == 0) break;
+      }
       const uint4 ch = cur;
       cur = nxt;
       if (c + 2 < nchunks) nxt = rc[(c + 2) * cs];
@@ -468,6 +481,7 @@ __global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
       }
     }
     if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+    early_final(dec, lp, lr);
   }
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
@@ -534,7 +548,12 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
     rd.init(a.r, a.nseq, q, a.N);
     RowCursor<S::NW, S::R> cur;
     cur.start(a, rd.peek());
+    int dec = 0;   // early decision (0 = open)
     for (int64_t t = 1; t <= a.N; ++t) {
+      if (a.early && t > 1 && ((t - 1) & (kEarlyEvery - 1)) == 0) {
+        if (!dec) dec = early_decide(lp, lr, a.N - (t - 1), a.lt_min, a.lp_min);
+        if (__ballot(dec == 0) == 0) break;
+      }
       {
         const uint32_t rr = rd.peek();
         const uint32_t rn = t < a.N ? rd.peek_next() : 0u;
@@ -604,6 +623,7 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
       }
     }
     if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+    early_final(dec, lp, lr);
   }
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
@@ -659,7 +679,12 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
     rd.init(a.r, a.nseq, q, a.N);
     RowCursor<NW, R> cur;
     cur.start(a, rd.peek());
+    int dec = 0;   // early decision (0 = open)
     for (int64_t t = 1; t <= a.N; ++t) {
+      if (a.early && t > 1 && ((t - 1) & (kEarlyEvery - 1)) == 0) {
+        if (!dec) dec = early_decide(lp, lr, a.N - (t - 1), a.lt_min, a.lp_min);
+        if (__ballot(dec == 0) == 0) break;
+      }
       {
         const uint32_t rr = rd.peek();
         const uint32_t rn = t < a.N ? rd.peek_next() : 0u;
@@ -790,6 +815,7 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
       }
     }
     if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
+    early_final(dec, lp, lr);
   }
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
@@ -900,13 +926,14 @@ int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t
 }
 
 int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
-                             int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream) {
+                             int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream, bool early) {
   if (M.kind != 0 || !M.d_rec) { set_error("table path needs a dense (enumerated) model"); return CVD_E_UNSUPPORTED; }
   if (nseq <= 0) return CVD_OK;
   TabArgs a;
   const int R = 1 << M.dec.n;
   a.rec = M.d_rec; a.logp1 = M.d_logp1; a.ltref = M.d_ltref; a.n = M.dec.n;
   a.S = M.S; a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
+  a.early = early && !d_sums; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
   const size_t lds = (size_t)M.S * R * (sizeof(double) + sizeof(uint32_t)) + (R + 1) * sizeof(double);
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
   // LDS-resident compact model (16-bit records): 1024-thread blocks when it
@@ -958,7 +985,7 @@ int cvd::explicit_kernel_of(const cvd_model& M) {
 
 int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                                 int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
-                                void* stream, int variant) {
+                                void* stream, int variant, bool early) {
   ExpKernel kern = nullptr;
   const uint32_t* bmp = nullptr;
   const int which = select_explicit(M, variant, &kern, &bmp, d_trace != nullptr);
@@ -975,6 +1002,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   a.hmask = (uint32_t)(M.hcap - 1); a.fmask = (uint32_t)(M.fcap - 1); a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   a.trace = d_trace;
+  a.early = early && !d_sums && !d_trace; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
   if (which == CVD_KERNEL_BUTTERFLY_RTC) {
     void* args[] = {&a};
@@ -1013,6 +1041,10 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_bfly, M.bfly))) return rc;
   }
   M.device = device;
+  // smallest per-step log P̂1 (early decision bound): every row entry and, for
+  // sparse models, the unvisited-row value
+  M.lp_min = M.kind == 1 ? M.logp1_unseen : 0.0;
+  for (double v : M.logp1) M.lp_min = std::min(M.lp_min, v);
   // code-specialised butterfly kernel (cvd_rtc.cpp); without it the compiled
   // table-driven kernel runs (same results), and the reason is kept for
   // cvd_model_jit_status
@@ -1089,14 +1121,22 @@ extern "C" int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N
   }
   int rc = check_device(*model);
   if (rc) return rc;
+  const bool early = (path & CVD_DETECT_EARLY_DECISION) != 0;
+  path &= ~CVD_DETECT_EARLY_DECISION;
+  if (early && d_sums) {
+    set_error("early decision stops a trial once its decision is certain: per-trial sums need the full run");
+    return CVD_E_INVALID;
+  }
   if (path == CVD_PATH_AUTO) path = model->kind == 0 ? CVD_PATH_TABLE : CVD_PATH_EXPLICIT;
-  if (path == CVD_PATH_TABLE) return launch_detect_table(*model, d_r, N, nseq, n_h1, d_sums, d_counts, stream);
+  if (path == CVD_PATH_TABLE)
+    return launch_detect_table(*model, d_r, N, nseq, n_h1, d_sums, d_counts, stream, early);
   if (path == CVD_PATH_EXPLICIT || path == CVD_PATH_EXPLICIT_GENERIC || path == CVD_PATH_EXPLICIT_ORBIT ||
       path == CVD_PATH_EXPLICIT_BUTTERFLY)
     return launch_detect_explicit(*model, d_r, N, nseq, n_h1, d_sums, d_counts, nullptr, stream,
                                   path == CVD_PATH_EXPLICIT ? kExplicitBest
                                   : path == CVD_PATH_EXPLICIT_ORBIT ? kExplicitOrbit
-                                  : path == CVD_PATH_EXPLICIT_BUTTERFLY ? kExplicitButterfly : kExplicitGeneric);
+                                  : path == CVD_PATH_EXPLICIT_BUTTERFLY ? kExplicitButterfly : kExplicitGeneric,
+                                  early);
   set_error("unknown path");
   return CVD_E_INVALID;
 }

@@ -258,9 +258,14 @@ class Detector:
                                            int(q0), int(count), _stream_ptr(stream)))
         return out
 
-    def detect(self, model, r, N, nseq, n_h1, sums=None, counts=None, path=_lib.PATH_AUTO, stream=None):
+    def detect(self, model, r, N, nseq, n_h1, sums=None, counts=None, path=_lib.PATH_AUTO, stream=None,
+               early_decision=False):
+        """early_decision: counts only; a trial stops once its decision is certain
+        (CVD_DETECT_EARLY_DECISION; same counts, no sums)."""
         if counts is None:
             counts = torch.zeros(2, dtype=torch.int64, device=self.device)
+        if early_decision:
+            path = int(path) | _lib.DETECT_EARLY_DECISION
         _lib.check(_lib.lib().cvd_detect(model.handle, ctypes.c_void_p(r.data_ptr()), int(N), int(nseq),
                                          int(n_h1),
                                          ctypes.c_void_p(sums.data_ptr() if sums is not None else 0),
@@ -292,10 +297,13 @@ class Detector:
         return int(max(1, min(trial_count, b)))
 
     def run_trials(self, model, gen1, gen2, N, p, seed, trial_begin, trial_end, batch=None,
-                   path=_lib.PATH_AUTO, return_sums=False, counts=None, stream=None):
+                   path=_lib.PATH_AUTO, return_sums=False, counts=None, stream=None, early_decision=False):
         """Global trials [trial_begin, trial_end) of one (N, p) grid point
         (Pd_plotter.py:198-223).  Returns {"counts": (s1, s2), "sums": [T, 4]?}
-        with sums per trial = (logp1, logp1_ref, logp2, logp2_ref)."""
+        with sums per trial = (logp1, logp1_ref, logp2, logp2_ref).
+        early_decision (counts only): stop each trial once its decision is certain."""
+        if early_decision and return_sums:
+            raise ValueError("early_decision gives counts only; per-trial sums need the full run")
         g1 = as_code(gen1, self.m, self.k, self.n)
         g2 = as_code(gen2, self.m, self.k, self.n)
         T = int(trial_end) - int(trial_begin)
@@ -308,10 +316,11 @@ class Detector:
         if not return_sums:
             wsz = lib.cvd_mc_workspace_bytes(g1.c, int(N), batch)
             work = torch.empty(max(wsz, 4) // 4, dtype=torch.int32, device=self.device)
+            flags = _lib.DETECT_EARLY_DECISION if early_decision else 0
             _lib.check(lib.cvd_mc_run(model.handle, g1.c, g2.c, float(p), int(N),
                                       int(seed) & 0xFFFFFFFFFFFFFFFF, int(trial_begin), int(trial_end),
                                       batch, ctypes.c_void_p(work.data_ptr()),
-                                      ctypes.c_void_p(counts.data_ptr()), int(path), _stream_ptr(stream)))
+                                      ctypes.c_void_p(counts.data_ptr()), int(path) | flags, _stream_ptr(stream)))
             return {"counts": counts}
         tag = grid_tag(N, p)
         out = []
@@ -341,12 +350,14 @@ def _detector(k, n, m, gen1, device=None):
 
 
 def run_experiment(k, n, m, gen1, gen2, num_iter, p_vec, learn_len, learn_burn, laplace, seed,
-                   N_list=None, device=None, batch=None, path=_lib.PATH_AUTO):
+                   N_list=None, device=None, batch=None, path=_lib.PATH_AUTO, early_decision=True):
     """Drop-in for Pd_plotter.run_experiment (Pd_plotter.py:176-235).
 
     Extra keyword arguments: N_list (defaults to the reference's
     N_SPECTRUM_BY_M.get(m, [50, 100, 200]), Pd_plotter.py:196), device, batch,
-    path.  When a torch.distributed default group is initialised (one process
+    path, early_decision (default on: the table needs only each trial's
+    decision, so a trial stops once it is certain -- identical Pd/Pc, see
+    CVD_DETECT_EARLY_DECISION).  When a torch.distributed default group is initialised (one process
     per GPU), trials are sharded by global trial id over the ranks and the
     success counts reduced with ONE all_reduce (RCCL on ROCm); every rank
     returns the same DataFrame.
@@ -361,7 +372,8 @@ def run_experiment(k, n, m, gen1, gen2, num_iter, p_vec, learn_len, learn_burn, 
 
     def count_fn(iN, N, ip, p, lo, hi, out):
         model = det.model(p, learn_len, learn_burn, laplace, seed)
-        det.run_trials(model, gen1, gen2, N, p, seed, lo, hi, batch=batch, path=path, counts=out)
+        det.run_trials(model, gen1, gen2, N, p, seed, lo, hi, batch=batch, path=path, counts=out,
+                       early_decision=early_decision)
 
     counts = run_sharded(count_fn, N_spectrum, list(p_vec), num_iter, det.device)
     return pd.DataFrame(pd_rows(counts, N_spectrum, list(p_vec), num_iter))

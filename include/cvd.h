@@ -155,6 +155,13 @@ int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int
 #define CVD_PATH_EXPLICIT_GENERIC 3  /* explicit path, ACS for every received word (no orbit reduction) */
 #define CVD_PATH_EXPLICIT_ORBIT 4    /* explicit path, k=1 two-representative orbit kernel */
 #define CVD_PATH_EXPLICIT_BUTTERFLY 5  /* explicit path, k=1 n=2 butterfly kernel, table-driven (not code-specialised) */
+/* OR'ed into `path` (cvd_detect, cvd_mc_run): early decision.  A trial's decision
+ * (Pd_plotter.py:215, :222) compares only its final sums; every log P̂1 and log T_ref
+ * increment lies in [min, 0], so once the running sums are far enough apart the
+ * outcome is certain (with a rigorous IEEE rounding margin) and a wavefront whose
+ * lanes have all decided stops.  Counts are identical to the full run; per-trial
+ * sums are then not produced (d_sums must be NULL). */
+#define CVD_DETECT_EARLY_DECISION 0x100
 
 /* Detector over sequences 0..nseq-1 (pitch = nseq): per sequence the sequential
  * fp64 sums log P̂1(D_0^N) and log T_ref(D_0^N) (Pd_plotter.py:106-116); sequences
