@@ -647,7 +647,7 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
     const int64_t L = prm->learn_len < 0 ? std::max<int64_t>(5000, 200 * S) : prm->learn_len;
     Mo->learn_len_eff = L;
     std::vector<int64_t> cnt((size_t)S * R, 0);
-    if (device >= 0) {
+    if (device >= 0 && L >= 1) {   // (an empty chain, L = 0, has nothing to run)
       rc = device_learn_dense(Mo->dec, next, S, L, prm->learn_burn, seed, prm->p, device, stream, cnt, stats);
       if (rc) return rc;
     } else {
@@ -699,7 +699,7 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
     std::vector<uint8_t> keys;
     StateMap map(M, &keys);
     std::vector<int64_t> cnt;
-    if (device >= 0) {
+    if (device >= 0 && L >= 1) {
       // the chain on the GPU: rows in first-visit order + counts; the host map is
       // rebuilt from the rows (insertion order = row order) for the successors
       std::vector<uint8_t> rows;
