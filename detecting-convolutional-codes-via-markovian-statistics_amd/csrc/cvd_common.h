@@ -96,6 +96,38 @@ CVD_HD uint32_t ctr_hi(uint64_t seq_id, uint32_t kind) {
 // thr(p) = floor(p * 2^32), p in [0, 1]; flip iff uniform < thr.
 inline uint64_t noise_threshold(double p) { return (uint64_t)(p * 4294967296.0); }
 
+// BSC flips of one received word, bit-sliced (spec: oracle/philox.py).  The
+// 32-bit uniform of word bit b is u_b = sum_i bit_b(P_i) 2^(31 - i) over the
+// word's 32 bit-planes P_i = word (i % 4) of
+// philox(ctr=(8 w + i / 4, seq_lo, ctr_hi(seq, kKindNoise), tag)), and bit b
+// flips iff u_b < thr.  The planes are compared with thr most significant first
+// for every bit at once: a bit is decided at the first plane where its uniform
+// bit differs from thr's (a 1 in thr over a 0 in u: flip), so the planes after
+// the last undecided bit are never drawn -- about 7 planes per word on one lane
+// instead of one uniform per code bit.  thr = 0 draws nothing (no flips),
+// thr = 2^32 flips every bit.
+constexpr int kNoisePlanes = 32, kNoiseBlocksPerWord = 8;
+
+// one plane: undecided bits U, flips F; thr bit tb of the plane
+CVD_HD void noise_plane(uint32_t r, uint32_t tb, uint32_t& U, uint32_t& F) {
+  if (tb) { F |= U & ~r; U &= r; }
+  else U &= ~r;
+}
+
+CVD_HD uint32_t noise_word(const StreamKey& key, uint64_t seq_id, uint64_t w, uint64_t thr, uint32_t valid) {
+  if (thr >= 4294967296ull) return valid;
+  uint32_t U = thr ? valid : 0u, F = 0u;
+  const uint32_t t = (uint32_t)thr, slo = (uint32_t)seq_id, nhi = ctr_hi(seq_id, kKindNoise);
+  for (int j = 0; j < kNoiseBlocksPerWord && U; ++j) {
+    const U4 x = philox((uint32_t)(w * kNoiseBlocksPerWord + (uint64_t)j), slo, nhi, key.tag, key.k0, key.k1);
+    noise_plane(x.x, (t >> (31 - 4 * j)) & 1u, U, F);
+    noise_plane(x.y, (t >> (30 - 4 * j)) & 1u, U, F);
+    noise_plane(x.z, (t >> (29 - 4 * j)) & 1u, U, F);
+    noise_plane(x.w, (t >> (28 - 4 * j)) & 1u, U, F);
+  }
+  return F;
+}
+
 // 32-bit tag of an (N, p) grid point (splitmix64 fold, top bit clear).
 inline uint32_t grid_tag(int64_t N, double p) {
   uint64_t bits;

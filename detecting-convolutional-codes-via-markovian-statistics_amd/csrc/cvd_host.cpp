@@ -281,19 +281,23 @@ struct HostStream {
   uint64_t thr;
   bool random_input;
   uint32_t s = 0;
-  int64_t nblk = -1, iblk = -1;
-  U4 nval{}, ival{};
+  int64_t nword = -1, iblk = -1;
+  uint32_t nmask = 0;
+  U4 ival{};
   HostStream(const CodeDesc& e, const Tabs& t, uint64_t seed, uint32_t tag, uint64_t sid,
              double p, bool ri)
       : enc(e), T(t), key{(uint32_t)seed, (uint32_t)(seed >> 32), tag}, seq_id(sid),
         thr(noise_threshold(p)), random_input(ri) {}
-  uint32_t noise_u(int64_t g) {
-    const int64_t b = g >> 2;
-    if (b != nblk) {
-      nval = philox((uint32_t)b, (uint32_t)seq_id, ctr_hi(seq_id, kKindNoise), key.tag, key.k0, key.k1);
-      nblk = b;
+  // flips of step t's n code bits: bits of received word t / spw (noise_word)
+  uint32_t noise_bits(int64_t t) {
+    const int spw = 32 / T.n;
+    const int64_t w = t / spw;
+    if (w != nword) {
+      const int nb = spw * T.n;
+      nmask = noise_word(key, seq_id, (uint64_t)w, thr, nb >= 32 ? ~0u : (1u << nb) - 1u);
+      nword = w;
     }
-    return u4_get(nval, (uint32_t)(g & 3));
+    return (nmask >> (uint32_t)((t - w * spw) * T.n)) & ((1u << T.n) - 1u);
   }
   uint32_t input_bit(int64_t bi) {
     const int64_t b = bi >> 7;
@@ -309,8 +313,7 @@ struct HostStream {
       for (int i = 0; i < T.k; ++i) U |= input_bit(t * T.k + i) << i;
     uint32_t r = T.out[s * T.K + U];
     s = T.nxt[s * T.K + U];
-    for (int j = 0; j < T.n; ++j) r ^= (uint32_t)((uint64_t)noise_u(t * T.n + j) < thr) << j;
-    return r;
+    return r ^ noise_bits(t);
   }
 };
 

@@ -96,23 +96,11 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
     }
     const int64_t t0 = w * spw;
     const int ns = (int)min((int64_t)spw, a.N - t0);
-    // BSC flips of the word's n*ns code bits (noise uniform g = t*n + j)
-    uint32_t nmask = 0;
-    const int64_t g0 = t0 * n, g1 = g0 + (int64_t)ns * n;
-    for (int64_t b = g0 >> 2; b <= ((g1 - 1) >> 2); ++b) {
-      // launder the (uniform) key so its 10-round schedule is recomputed by
-      // scalar adds per call instead of being hoisted into spilled SGPRs
-      uint32_t k0 = a.k0, k1 = a.k1;
-      asm volatile("" : "+s"(k0), "+s"(k1));
-      const U4 x = philox((uint32_t)b, slo, nhi, a.tag, k0, k1);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t g = 4 * b + e;
-        const uint32_t u = u4_get(x, e);
-        const uint32_t flip = a.thr_all ? 1u : (u < a.thr_lo ? 1u : 0u);
-        if (g >= g0 && g < g1) nmask |= flip << (uint32_t)(g - g0);
-      }
-    }
+    // BSC flips of the word's n*ns code bits (bit-sliced noise, noise_word)
+    const uint32_t valid = n * ns >= 32 ? ~0u : (1u << (uint32_t)(n * ns)) - 1u;
+    const StreamKey key{a.k0, a.k1, a.tag};
+    const uint32_t nmask = noise_word(key, sid, (uint64_t)w, a.thr_all ? 4294967296ull : (uint64_t)a.thr_lo, valid);
+    (void)nhi;
     // encoder input bits [t0*k, (t0+ns)*k) of the input stream
     uint32_t ib = 0;
     if (a.random_input) {
@@ -158,10 +146,12 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
 //    input bits, so every term is one shift of a window: output stream j is the
 //    XOR of W_r >> sh over the host-built tap set taps[j][r] (bit sh), and the
 //    n streams are bit-interleaved into the word (step i in bits n*i .. n*i+n-1).
-//  * Noise: a group of GW words spans whole Philox blocks (GW = 1 for n = 2,
-//    2 for n = 3); each flip u < thr is the borrow of u - thr, shifted into the
-//    word's mask by one add-with-carry (two VOP2 per code bit), highest uniform
-//    first so uniform g0 + i lands on bit i.
+//  * Noise: bit-sliced (noise_word, cvd_common.h): the word's bit-planes are
+//    compared with thr for all of its code bits at once, most significant first.
+//    The first three Philox blocks (12 planes) run as one interleaved group; then
+//    one block at a time while any lane of the wave still has an undecided bit
+//    (the wave needs ~3.4 blocks per word on average, against NBITS / 4 = 8 blocks
+//    of one uniform per code bit).
 template <int n>
 __device__ __forceinline__ uint32_t spread_n(uint32_t x) {   // bit i -> bit n*i
   if constexpr (n == 1) {
@@ -190,19 +180,54 @@ __device__ __forceinline__ uint32_t even_bits(uint32_t x) {   // bit 2i -> bit i
   return (x | (x >> 8)) & 0x0000FFFFu;
 }
 
-__device__ __forceinline__ uint32_t shift_in_flip(uint32_t mask, uint32_t u, uint32_t thr) {
-  uint32_t t;
-  asm volatile("v_subrev_co_u32_e32 %0, vcc, %2, %3\n\t"
-               "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
-               : "=&v"(t), "+v"(mask) : "s"(thr), "v"(u) : "vcc");
-  return mask;
+// One bit-plane with thr's bit as a uniform mask pm (0 or ~0): noise_plane
+// without a select, two v_bitop3 (pm in an SGPR) and an or.
+__device__ __forceinline__ void noise_plane_m(uint32_t r, uint32_t pm, uint32_t& U, uint32_t& F) {
+  F |= U & ~r & pm;
+  U &= ~(r ^ pm);
+}
+
+// Flip mask of received word w of one sequence (noise_word's spec) for the wave:
+// thr (< 2^32, > 0) and the key uniform; valid = the word's code bits.
+__device__ __forceinline__ uint32_t noise_word_wave(const GenArgs& a, uint32_t slo, uint32_t nhi, uint32_t w,
+                                                    uint32_t valid) {
+  const uint32_t t = a.thr_lo;
+  uint32_t U = valid, F = 0u;
+  {
+    // launder the (uniform) key so its 10-round schedule is recomputed by scalar
+    // adds per group instead of being hoisted into SGPRs
+    uint32_t k0 = a.k0, k1 = a.k1;
+    asm volatile("" : "+s"(k0), "+s"(k1));
+    uint32_t xv[3][4];
+#pragma unroll
+    for (int gb = 0; gb < 3; ++gb) {
+      xv[gb][0] = w * kNoiseBlocksPerWord + (uint32_t)gb; xv[gb][1] = slo; xv[gb][2] = nhi; xv[gb][3] = a.tag;
+    }
+    philox_blocks<3>(xv, k0, k1);
+#pragma unroll
+    for (int gb = 0; gb < 3; ++gb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) noise_plane_m(xv[gb][e], 0u - ((t >> (31 - 4 * gb - e)) & 1u), U, F);
+  }
+#pragma nounroll
+  for (int j = 3; j < kNoiseBlocksPerWord; ++j) {
+    if (__ballot(U != 0u) == 0ull) break;   // every bit of every lane decided
+    uint32_t k0 = a.k0, k1 = a.k1;
+    asm volatile("" : "+s"(k0), "+s"(k1));
+    const U4 x = philox(w * kNoiseBlocksPerWord + (uint32_t)j, slo, nhi, a.tag, k0, k1);
+    const uint32_t tj = t << (4 * j);   // thr bits 31 - 4j .. 28 - 4j at the top
+    noise_plane_m(x.x, (uint32_t)((int32_t)tj >> 31), U, F);
+    noise_plane_m(x.y, (uint32_t)((int32_t)(tj << 1) >> 31), U, F);
+    noise_plane_m(x.z, (uint32_t)((int32_t)(tj << 2) >> 31), U, F);
+    noise_plane_m(x.w, (uint32_t)((int32_t)(tj << 3) >> 31), U, F);
+  }
+  return F;
 }
 
 template <int k, int n>
 __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   constexpr int SPW = 32 / n, NBITS = SPW * n;
-  constexpr int GW = (NBITS % 4 == 0) ? 1 : (NBITS % 2 == 0) ? 2 : 4;
-  constexpr int NB = GW * NBITS / 4;          // Philox blocks per group
+  constexpr uint32_t kValid = NBITS == 32 ? ~0u : (1u << NBITS) - 1u;
   static_assert(k >= 1 && k <= 2 && SPW * k <= 32, "gen_fast_kernel: shape");
   const int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (li >= a.count) return;
@@ -257,82 +282,45 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   for (int64_t w4 = 4 * c0; w4 < 4 * c1; w4 += 4) {
     uint32_t out4[4];
 #pragma unroll
-    for (int g = 0; g < 4; g += GW) {
-      const int64_t wg = w4 + g;
-      uint32_t nm[GW];
+    for (int g = 0; g < 4; ++g) {
+      const int64_t w = w4 + g;
+      uint32_t word = 0u;
+      if (w < nwords) {
+        const uint32_t nm = a.thr_all ? kValid : a.thr_lo ? noise_word_wave(a, slo, nhi, (uint32_t)w, kValid) : 0u;
+        uint32_t U[k];
+        word_inputs(w, U);
+        uint32_t Wr[k];
 #pragma unroll
-      for (int e = 0; e < GW; ++e) nm[e] = 0u;
-      if (wg < nwords) {
-        if (a.thr_all) {
-#pragma unroll
-          for (int e = 0; e < GW; ++e) nm[e] = ~0u;
-        } else {
-          const uint32_t b0 = (uint32_t)(wg * NBITS / 4);
-          // blocks in groups of kPG: the group's Philox chains are independent
-          // (interleaved by the scheduler), then its flips shift in, highest first
-          constexpr int kPG = NB % 4 == 0 ? 4 : NB % 3 == 0 ? 3 : 1;
-#pragma unroll
-          for (int g0 = NB - kPG; g0 >= 0; g0 -= kPG) {
-            // launder the (uniform) key so its 10-round schedule is recomputed
-            // by scalar adds per group instead of being hoisted into SGPRs
-            uint32_t k0 = a.k0, k1 = a.k1;
-            asm volatile("" : "+s"(k0), "+s"(k1));
-            uint32_t xv[kPG][4];
-#pragma unroll
-            for (int gb = 0; gb < kPG; ++gb) {
-              xv[gb][0] = b0 + (uint32_t)(g0 + gb); xv[gb][1] = slo; xv[gb][2] = nhi; xv[gb][3] = a.tag;
-            }
-            philox_blocks<kPG>(xv, k0, k1);
-#pragma unroll
-            for (int gb = kPG - 1; gb >= 0; --gb)
-#pragma unroll
-              for (int e = 3; e >= 0; --e) {
-                const int ew = (4 * (g0 + gb) + e) / NBITS;
-                nm[ew] = shift_in_flip(nm[ew], xv[gb][e], a.thr_lo);
-              }
-          }
+        for (int r = 0; r < k; ++r) {
+          Wr[r] = (U[r] << hs) | hist[r];
+          hist[r] = (Wr[r] >> SPW) & hmask;
         }
-      }
 #pragma unroll
-      for (int e = 0; e < GW; ++e) {
-        const int64_t w = wg + e;
-        uint32_t word = 0u;
-        if (w < nwords) {
-          uint32_t U[k];
-          word_inputs(w, U);
-          uint32_t Wr[k];
+        for (int j = 0; j < n; ++j) {
+          uint32_t o = 0u;
 #pragma unroll
           for (int r = 0; r < k; ++r) {
-            Wr[r] = (U[r] << hs) | hist[r];
-            hist[r] = (Wr[r] >> SPW) & hmask;
-          }
-#pragma unroll
-          for (int j = 0; j < n; ++j) {
-            uint32_t o = 0u;
-#pragma unroll
-            for (int r = 0; r < k; ++r) {
-              // the set taps only, as a scalar loop over the uniform mask (s_ff1):
-              // two VALU per tap.  The mask is re-read per word -- hoisted out of
-              // the chunk loop, per-shift conditions filled the SGPRs (spills) and
-              // unrolled they became selects for every possible shift
-              uint32_t tm = a.taps[j][r];
-              asm volatile("" : "+s"(tm));
+            // the set taps only, as a scalar loop over the uniform mask (s_ff1):
+            // two VALU per tap.  The mask is re-read per word -- hoisted out of
+            // the chunk loop, per-shift conditions filled the SGPRs (spills) and
+            // unrolled they became selects for every possible shift
+            uint32_t tm = a.taps[j][r];
+            asm volatile("" : "+s"(tm));
 #pragma nounroll
-              while (tm) {
-                const uint32_t sh = (uint32_t)__builtin_ctz(tm);
-                tm &= tm - 1u;
-                o ^= Wr[r] >> sh;
-              }
+            while (tm) {
+              const uint32_t sh = (uint32_t)__builtin_ctz(tm);
+              tm &= tm - 1u;
+              o ^= Wr[r] >> sh;
             }
-            if constexpr (SPW < 32) o &= (1u << SPW) - 1u;
-            word |= spread_n<n>(o) << j;
           }
-          word ^= nm[e];
-          const int64_t ns = a.N - w * SPW;           // steps in this word (last word: < SPW)
-          if (ns < SPW) word &= (1u << (n * ns)) - 1u;
+          if constexpr (SPW < 32) o &= (1u << SPW) - 1u;
+          word |= spread_n<n>(o) << j;
         }
-        out4[g + e] = word;
+        word ^= nm;
+        const int64_t ns = a.N - w * SPW;           // steps in this word (last word: < SPW)
+        if (ns < SPW) word &= (1u << (n * ns)) - 1u;
       }
+      out4[g] = word;
     }
     *reinterpret_cast<uint4*>(a.r + chunk_index(w4 >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
   }

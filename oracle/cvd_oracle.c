@@ -150,12 +150,12 @@ static int64_t idx_insert(Index* I, const uint8_t* k, int* ins) {
 /* ───────────────────────── simulator spec ────────────────────────────────── */
 typedef struct {
   const Tabs* T; uint32_t k0, k1, tag; uint64_t sid, thr; int s;
-  int64_t nb, ib; uint32_t nv[4], iv[4];
+  int64_t nw, ib; uint32_t nmask, iv[4], iv_noise[4];
 } Stream;
 
 static void stream_init(Stream* S, const Tabs* T, uint64_t seed, uint32_t tag, uint64_t sid, double p) {
   S->T = T; S->k0 = (uint32_t)seed; S->k1 = (uint32_t)(seed >> 32); S->tag = tag; S->sid = sid;
-  S->thr = (uint64_t)(p * 4294967296.0); S->s = 0; S->nb = -1; S->ib = -1;
+  S->thr = (uint64_t)(p * 4294967296.0); S->s = 0; S->nw = -1; S->ib = -1;
 }
 static uint32_t chi(uint64_t sid, uint32_t kind) { return (uint32_t)((sid >> 32) & 0xFFFF) | (kind << 16); }
 static int stream_next(Stream* S, int64_t t) {
@@ -171,14 +171,29 @@ static int stream_next(Stream* S, int64_t t) {
   }
   int r = T->out[S->s * T->K + U];
   S->s = T->nxt[S->s * T->K + U];
-  for (int j = 0; j < T->n; ++j) {
-    int64_t g = t * T->n + j, blk = g >> 2;
-    if (blk != S->nb) {
-      S->nv[0] = (uint32_t)blk; S->nv[1] = (uint32_t)S->sid; S->nv[2] = chi(S->sid, 0); S->nv[3] = S->tag;
-      philox(S->nv, S->k0, S->k1); S->nb = blk;
+  /* BSC flips, bit-sliced (oracle/philox.py noise_bits): the uniform of bit b of
+     received word w is sum_i bit_b(P_i) 2^(31-i) over the bit-planes
+     P_i = word i%4 of philox(8w + i/4, ...); decided plane by plane, MSB first */
+  const int spw = 32 / T->n, nb = spw * T->n;
+  const int64_t w = t / spw;
+  if (w != S->nw) {
+    uint32_t und = nb >= 32 ? 0xFFFFFFFFu : (1u << nb) - 1u, flp = 0;
+    if (S->thr >= 4294967296ull) flp = und, und = 0;
+    if (S->thr == 0) und = 0;
+    for (int i = 0; i < 32 && und; ++i) {
+      if ((i & 3) == 0) {
+        uint32_t c[4];
+        c[0] = (uint32_t)(w * 8 + i / 4); c[1] = (uint32_t)S->sid; c[2] = chi(S->sid, 0); c[3] = S->tag;
+        philox(c, S->k0, S->k1);
+        memcpy(S->iv_noise, c, sizeof c);
+      }
+      const uint32_t pl = S->iv_noise[i & 3];
+      if ((S->thr >> (31 - i)) & 1u) { flp |= und & ~pl; und &= pl; }
+      else und &= ~pl;
     }
-    r ^= ((uint64_t)S->nv[g & 3] < S->thr) << j;
+    S->nmask = flp; S->nw = w;
   }
+  r ^= (int)((S->nmask >> ((t - w * spw) * T->n)) & ((1u << T->n) - 1u));
   return r;
 }
 

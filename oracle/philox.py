@@ -22,10 +22,17 @@ csrc/cvd_common.h):
   (hyp 0 = H1 stream encoded with G1, hyp 1 = H2 stream encoded with G2) and
   tag = grid_tag(N, p).  The P̂1 learning chain uses seq_id = 0 and
   tag = LEARN_TAG.
-* noise: the uniform for output bit j of step t is word (g % 4) of
-  philox(ctr=(g // 4, seq_lo, seq_hi16 | KIND_NOISE << 16, tag)) with
-  g = t*n + j; the bit flips iff uniform < thr(p), thr(p) = floor(p * 2^32)
-  (p == 1.0 -> 2^32, i.e. always).
+* noise (bit-sliced): received word w of a sequence holds steps
+  [w*spw, (w+1)*spw), spw = 32 // n, step i of the word in bits [n*i, n*i+n)
+  (output bit j of step t is word bit b = (t % spw)*n + j).  The word has 32
+  bit-planes P_0..P_31, P_i = word (i % 4) of
+  philox(ctr=(8*w + i // 4, seq_lo, seq_hi16 | KIND_NOISE << 16, tag)).  The
+  32-bit uniform of word bit b is u_b = sum_i bit_b(P_i) * 2^(31 - i), and the
+  bit flips iff u_b < thr(p), thr(p) = floor(p * 2^32) (p == 1.0 -> 2^32, i.e.
+  always).  Implementations compare the planes with thr most significant first
+  for all bits of the word at once and stop drawing planes once every bit is
+  decided (the first plane where u_b and thr differ decides it); the result is
+  the same as drawing all 32.
 * inputs: input bit i of step t is bit (b % 32) of word ((b // 32) % 4) of
   philox(ctr=(b // 128, seq_lo, seq_hi16 | KIND_INPUT << 16, tag)) with
   b = t*k + i (all zero when random_input=False).
@@ -87,16 +94,31 @@ def _ctr_hi(seq_id, kind):
     return ((int(seq_id) >> 32) & 0xFFFF) | (kind << 16)
 
 
-def noise_bits(seed, tag, seq_id, N, n, p):
-    """(N, n) uint8 array of BSC flips for one sequence."""
-    g = np.arange(N * n, dtype=np.uint64)
-    blk = g // 4
-    w = (g % 4).astype(np.int64)
+def noise_word_uniforms(seed, tag, seq_id, w, n):
+    """(len(w), 32) uint64 array: the uniforms u_b of word bits b = 0..31 of
+    received words `w` (bits b >= spw*n are defined but unused)."""
+    w = np.asarray(w, dtype=np.uint64)
+    blk = (w[:, None] * np.uint64(8) + np.arange(8, dtype=np.uint64)[None, :]).reshape(-1)
     x = philox4x32_10(blk, np.full_like(blk, int(seq_id) & MASK32),
                       np.full_like(blk, _ctr_hi(seq_id, KIND_NOISE)),
                       np.full_like(blk, tag), seed & MASK32, seed >> 32)
-    u = np.choose(w, x).astype(np.uint64)
-    return (u < np.uint64(threshold(p))).astype(np.uint8).reshape(N, n)
+    planes = np.stack(x, axis=1).reshape(len(w), 32).astype(np.uint64)    # plane i = block i//4, word i%4
+    bits = (planes[:, :, None] >> np.arange(32, dtype=np.uint64)[None, None, :]) & np.uint64(1)
+    weights = (np.uint64(1) << (np.uint64(31) - np.arange(32, dtype=np.uint64)))[None, :, None]
+    return (bits * weights).sum(axis=1, dtype=np.uint64)
+
+
+def noise_bits(seed, tag, seq_id, N, n, p):
+    """(N, n) uint8 array of BSC flips for one sequence."""
+    spw = 32 // n
+    nwords = (N + spw - 1) // spw
+    thr = np.uint64(threshold(p))
+    out = np.zeros((nwords, spw * n), np.uint8)
+    for c0 in range(0, nwords, 4096):                  # bounded memory: (words, 32, 32) per chunk
+        ws = np.arange(c0, min(nwords, c0 + 4096))
+        u = noise_word_uniforms(seed, tag, seq_id, ws, n)[:, :spw * n]
+        out[c0:c0 + len(ws)] = (u < thr).astype(np.uint8)
+    return out.reshape(nwords * spw, n)[:N]
 
 
 def input_bits(seed, tag, seq_id, N, k):

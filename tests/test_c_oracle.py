@@ -23,6 +23,39 @@ def test_c_stream_matches_spec(golden, name, N, p):
                                       R.received_stream(taps, m, k, n, N, p, 77, tag, sid))
 
 
+@pytest.mark.parametrize("p", [0.0, 1.0, 0.5, 2.0 ** -32, 0.25 + 2.0 ** -32, 1 - 2.0 ** -32, 0.0033, 0.2])
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_noise_spec_edges(n, p):
+    """Bit-sliced noise: the C oracle's early-exit plane comparison equals the
+    numpy spec (all 32 planes composed into uniforms) at threshold edge cases
+    (thr = 0, 2^32, powers of two, a single low bit, all ones)."""
+    taps = {1: [[[1, 1, 1]]], 2: [[[1, 1, 1]], [[1, 0, 1]]], 3: [[[1, 1, 1]], [[1, 0, 1]], [[0, 1, 1]]]}[n]
+    N = 701
+    tag = philox.grid_tag(N, p)
+    for sid in (0, 3):
+        np.testing.assert_array_equal(C.stream(C.Code(taps, 2, 1, n), N, p, 99, tag, sid),
+                                      R.received_stream(taps, 2, 1, n, N, p, 99, tag, sid))
+
+
+def test_noise_spec_definition():
+    """noise_bits against the spec's definition written out bit by bit with Python ints."""
+    seed, tag, sid, n, N, p = 5, 17, 9, 2, 40, 0.3
+    thr = philox.threshold(p)
+    got = philox.noise_bits(seed, tag, sid, N, n, p)
+    for w in range(N // 16 + 1):
+        planes = []
+        for j in range(8):
+            x = philox.philox4x32_10([8 * w + j], [sid], [philox._ctr_hi(sid, philox.KIND_NOISE)], [tag],
+                                     seed, 0)
+            planes += [int(v[0]) for v in x]
+        for b in range(32):
+            t, jb = divmod(w * 32 + b, n)
+            if t >= N:
+                continue
+            u = sum(((planes[i] >> b) & 1) << (31 - i) for i in range(32))
+            assert got[t, jb] == (u < thr)
+
+
 @pytest.mark.parametrize("ename", ["exp_m2_75_57", "exp_m3_demo"])
 def test_c_oracle_sums_vs_reference(golden, ename):
     z, meta = golden
