@@ -24,8 +24,6 @@ namespace cvd_dev {
 using cvd::kEmptyKey;
 using cvd::row_words_c;
 using cvd::key_hash;
-using cvd::filter_mix;
-using cvd::filter_bits;
 
 constexpr int kBlock = 256;
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -135,9 +133,10 @@ constexpr int kEarlyEvery = 128;   // steps between checks (the k = 1 butterfly 
 // ────────────────────────── explicit metric path ────────────────────────────
 
 struct ExpArgs {
-  const uint32_t* filt;     // [fmask + 1] Bloom filter words over the row keys (filter_bits)
+  const uint32_t* filt;     // [fmask + 1] Bloom filter words over the row keys (filter_pattern)
   const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors, word 0 = kEmptyKey if empty
-  const uint32_t* hrow;     // [hcap][row_words(n)]: log P̂1[r] (f64), successor slot[r] (i32, -1 = not a row)
+  const uint32_t* hrow;     // [hcap][row_words(n)]: log P̂1[r] (f64), successor row[r] (i32, -1 = not a row)
+  const uint32_t* drow;     // [rows][row_words(n)]: the same records dense by row id (table mode)
   const double* ltref;      // [R + 1]
   const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
@@ -145,7 +144,7 @@ struct ExpArgs {
   uint32_t bfly_even[4];    // k = 1 butterfly kernel: nibble masks of the butterflies with out(j, 0) in {00, 11}
   uint32_t hmask, fmask;
   int32_t max_probe;
-  int32_t slot0;            // slot of D_0 = 0
+  int32_t slot0;            // row of D_0 = 0
   double lp_unseen;
   int64_t N, nseq, n_h1;
   const uint32_t* r;
@@ -187,16 +186,6 @@ struct StreamReader {
   }
 };
 
-// Lookup of the P̂1 row of the current metric state.  A learned row stores the
-// slot of its successor for every received word, so a sequence that stays in
-// learned states walks rows with one small prefetched load per step and no
-// hashing ("table mode").  After an unvisited state the successor is unknown
-// and the next state is hashed: its Bloom-filter word is fetched one step
-// ahead (L2-resident; a negative answer -- almost every non-row -- ends the
-// lookup), the key and row entries of the home slot only on a positive answer
-// (mid-step), and the exact key compare, with linear probing past an occupied
-// home slot, happens when the step resolves.  slot: >= 0 known row, -1 known
-// unvisited row, -2 pending hash probe (home slot hs, filter word fw, bit mix h3).
 // 32-bit byte offsets from a uniform base (global_load with an SGPR base: no
 // 64-bit address arithmetic per lane)
 template <typename T>
@@ -204,21 +193,58 @@ __device__ __forceinline__ T ld_off(const void* base, uint32_t byte_off) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
+// Bloom-filter bit patterns (cvd_keys.h filter_pattern) in LDS: one table per
+// workgroup, filled at kernel start (fill_filter_patterns + __syncthreads).
+__device__ __forceinline__ uint32_t* filter_patterns_lds() {
+  __shared__ uint32_t s_pat[cvd::kFilterPatterns];
+  return s_pat;
+}
+__device__ __forceinline__ void fill_filter_patterns() {
+  uint32_t* t = filter_patterns_lds();
+  for (int i = threadIdx.x; i < cvd::kFilterPatterns; i += blockDim.x) t[i] = cvd::filter_pattern((unsigned)i);
+}
+
+// Ablation knobs for timing studies only (profiles/ab_k1b.py --no-check; results
+// differ): bit 0 drops the P̂1 row lookup, bit 1 the T_ref count, bit 2 the
+// hashed lookup of states outside the learned rows (table mode only).
+#ifndef CVD_ABL
+#define CVD_ABL 0
+#endif
+
+// Lookup of the P̂1 row of the current metric state.  A learned row's record
+// holds the row of its successor for every received word, so a sequence that
+// stays in learned states walks the dense row-indexed records with one small
+// prefetched load per step and no hashing ("table mode").  After an unvisited
+// state the successor is unknown and the next state is hashed: its Bloom-filter
+// word is fetched one step ahead (L2-resident; a negative answer -- almost
+// every non-row -- ends the lookup) together with its bit pattern (LDS), the
+// key and the directory record of the home slot only on a positive answer
+// (mid-step), and the exact key compare, with linear probing past an occupied
+// home slot, happens when the step resolves.  slot: >= 0 known row id, -1 known
+// unvisited row, -2 pending hash probe (home slot hs, filter word fw, pattern fb).
 template <int NW, int R>
 struct RowCursor {
   static constexpr uint32_t RSB = 4u * row_words_c(R);   // record bytes
   int32_t slot, pnx;
-  uint32_t hs, h3, fw;
+  uint32_t hs, fb, fw;
   bool cand;
   double plp;
   uint32_t pkey[NW];
+  // record entries (log P̂1, successor row) of row s (dense records, table mode)
+  // or of directory slot s (a hashed lookup's hit) for word rn
   __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
+    const uint32_t off = (uint32_t)s * RSB;
+    plp = ld_off<double>(a.drow, off + 8u * rn);
+    pnx = ld_off<int32_t>(a.drow, off + 4u * (2u * R + rn));
+  }
+  __device__ void prefetch_dir(const ExpArgs& a, int32_t s, uint32_t rn) {
     const uint32_t off = (uint32_t)s * RSB;
     plp = ld_off<double>(a.hrow, off + 8u * rn);
     pnx = ld_off<int32_t>(a.hrow, off + 4u * (2u * R + rn));
   }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
-    slot = a.slot0; hs = 0u; h3 = 0u; fw = 0u; cand = false;
+    slot = a.slot0; hs = 0u; fb = 0u; fw = 0u; cand = false;
+    if (CVD_ABL & 1) return;
     prefetch_row(a, slot, r0);
   }
   // Ordering fences: nothing in mid() / resolve() depends on the ACS, so
@@ -236,12 +262,12 @@ struct RowCursor {
     for (int w = 0; w < N_; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
   }
   __device__ void mid(const ExpArgs& a, uint32_t r) {
-    const uint32_t fb = filter_bits(h3);
+    if (CVD_ABL & 1) return;
     cand = slot == -2 && (fw & fb) == fb;
     if (cand) {
 #pragma unroll
       for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs * NW + w) * 4u);
-      prefetch_row(a, (int32_t)hs, r);
+      prefetch_dir(a, (int32_t)hs, r);
     }
   }
   __device__ static bool same_key(const uint32_t (&x)[NW], const uint32_t (&y)[NW]) {
@@ -259,6 +285,7 @@ struct RowCursor {
   // or hashed
   __device__ double resolve(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t r, uint32_t kmu8 = 0u) {
     double lpv = a.lp_unseen;
+    if (CVD_ABL & 1) return lpv;
     int32_t ns = -2;
     if (slot >= 0) {
       lpv = plp; ns = pnx;
@@ -291,17 +318,18 @@ struct RowCursor {
   }
   // D_t's key is known: issue the next step's loads
   __device__ void prefetch(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t rn, uint32_t kmu8 = 0u) {
+    if (CVD_ABL & 1) return;
     if (slot >= 0) {
       prefetch_row(a, slot, rn);
-    } else if (slot == -2) {
+    } else if (slot == -2 && !(CVD_ABL & 4)) {
       uint32_t key[NW];
 #pragma unroll
       for (int w = 0; w < NW; ++w) key[w] = key_in[w] - kmu8;
-      uint32_t h1, h2;
-      key_hash(key, NW, h1, h2);
-      hs = h1 & a.hmask;
-      h3 = filter_mix(h1, h2);
-      fw = ld_off<uint32_t>(a.filt, (h2 & a.fmask) * 4u);
+      uint32_t ph, pl;
+      key_hash(key, NW, ph, pl);
+      hs = ph & a.hmask;
+      fb = filter_patterns_lds()[cvd::filter_pattern_index(pl)];
+      fw = ld_off<uint32_t>(a.filt, (pl & a.fmask) * 4u);
     }
   }
 };
@@ -473,6 +501,24 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
   for (int j = 0; j < H; ++j) Dp[j] = E[j];
 }
 
+// Butterfly parity classes of a specialised code (out(j, 0) = bits 2j..2j+1 of
+// XM), as cvd_host.cpp build_bfly derives them at run time: every out(j, 0) of
+// even parity (bfly_uni), and the nibble mask of the even-parity butterflies of
+// halves-difference word v (bfly_even[v], device key layout).
+template <int m, uint64_t XM>
+__device__ constexpr bool xm_uni() {
+  for (int j = 0; j < (1 << m) / 2; ++j)
+    if (__builtin_popcount((unsigned)((XM >> (2 * j)) & 3u)) & 1) return false;
+  return true;
+}
+template <int m, uint64_t XM>
+__device__ constexpr uint32_t xm_even(int v) {
+  uint32_t w = 0u;
+  for (int j = 8 * v; j < 8 * v + 8 && j < (1 << m) / 2; ++j)
+    if (!(__builtin_popcount((unsigned)((XM >> (2 * j)) & 3u)) & 1)) w |= 0xFu << (4 * cvd::key_nibble(1 << m, j));
+  return w;
+}
+
 template <int V>
 struct IntC {
   static constexpr int value = V;
@@ -484,6 +530,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
   static_assert(m >= 3, "k1b kernel: 2^m >= 8 (whole key words)");
   __shared__ double s_lt[R + 1];
   if (threadIdx.x <= R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  fill_filter_patterns();
   __syncthreads();
   // Sequence index without a VGPR live across the step loop: the wave's first
   // index in SGPRs, the lane from mbcnt, recomputed after the loop; validity
@@ -553,10 +600,11 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       // pair-swap test are those with out(j, 0) of y's parity
       const uint32_t pm = 0u - (uint32_t)(__builtin_popcount(rr) & 1u);
       uint32_t hx = 0u, sym = 0u;
+      constexpr bool kUniKnown = kSpec, kUni = kSpec && xm_uni<m, XM>();
 #pragma unroll
       for (int v = 0; v < NH; ++v) {
-        hx |= dh[v];
-        sym |= dh[v] & (a.bfly_even[v] ^ pm);
+        if (!kUniKnown || kUni) hx |= dh[v];
+        sym |= dh[v] & ((kSpec ? xm_even<m, XM>(v) : a.bfly_even[v]) ^ pm);
       }
       // D_t's key.  Lazy form: raw nibbles (canonical + mu in every nibble, no
       // borrow since mu = 1 means every nibble >= 1); the halves test only asks
@@ -565,7 +613,8 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       for (int v = 0; v < NW; ++v) key[v] = CVD_K1B_LAZYKEY ? kw[v] : kw[v] - mu8;
       kmu8 = CVD_K1B_LAZYKEY ? mu8 : 0u;
       // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni
-      const uint32_t c = 1u + (sym == 0u) + ((hx == 0u && a.bfly_uni) ? 2u : 0u);
+      const bool uni = kUniKnown ? kUni : a.bfly_uni != 0u;
+      const uint32_t c = (CVD_ABL & 2) ? 1u : 1u + (sym == 0u) + ((uni && hx == 0u) ? 2u : 0u);
       lr += s_lt[c];                          // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
       if constexpr (kTrace) {
         uint32_t ck[NW];

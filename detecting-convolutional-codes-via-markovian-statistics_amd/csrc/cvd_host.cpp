@@ -460,11 +460,15 @@ extern "C" int cvd_enumerate(const cvd_code* dec, int64_t cap, int64_t* S_out, u
 namespace {
 
 void build_hash(cvd_model& Mo) {
-  // Explicit-path row table: a Bloom filter over the row keys, and an
-  // open-addressing directory (linear probing) of the nibble-packed metric
-  // vectors with, per slot, the row record {log P̂1[r], slot of successor(r)
-  // or -1}.  The successor slots let a sequence walk learned rows without
-  // hashing (table mode); the filter ends most lookups of non-rows.
+  // Explicit-path row table:
+  //  * a blocked Bloom filter over the row keys (filter_pattern);
+  //  * an open-addressing directory (linear probing) of the nibble-packed metric
+  //    vectors with, per slot, the row's record {log P̂1[r], row of successor(r)
+  //    or -1} -- read when a hashed lookup hits;
+  //  * the same records dense by row id (h_drow), which a sequence walking
+  //    learned rows reads without hashing (table mode): the rows a walk visits
+  //    sit together in first-visit order instead of scattered over the
+  //    directory (load <= 1/8).
   const int m = Mo.dec.m, M = 1 << m, R = 1 << Mo.dec.n, nw = nib_words(m);
   int64_t cap = 64;
   while (cap < 8 * Mo.n_rows) cap <<= 1;   // load factor <= 1/8: a hit is at its home slot ~94% of the time
@@ -479,21 +483,22 @@ void build_hash(cvd_model& Mo) {
   Mo.h_key.assign((size_t)cap * nw, kEmptyKey);
   Mo.h_rsw = row_words(Mo.dec.n);
   Mo.h_row.assign((size_t)cap * Mo.h_rsw, 0u);
+  Mo.h_drow.assign((size_t)Mo.n_rows * Mo.h_rsw, 0u);
   Mo.max_probe = 0;
   std::vector<int64_t> slot_of((size_t)Mo.n_rows);
-  std::vector<uint32_t> kws((size_t)Mo.n_rows * nw), h1s((size_t)Mo.n_rows), h2s((size_t)Mo.n_rows);
+  std::vector<uint32_t> kws((size_t)Mo.n_rows * nw), phs((size_t)Mo.n_rows), pls((size_t)Mo.n_rows);
   parallel_for(Mo.n_rows, [&](int64_t i, int) {
     uint32_t* kw = kws.data() + (size_t)i * nw;
     pack_nibbles(Mo.keys.data() + (size_t)i * M, M, kw);
     if (M >= 8)
       for (int w = 0; w < nw; ++w) kw[w] = key_swap(kw[w]);   // device key layout
-    key_hash(kw, nw, h1s[(size_t)i], h2s[(size_t)i]);
+    key_hash(kw, nw, phs[(size_t)i], pls[(size_t)i]);
   });
   for (int64_t i = 0; i < Mo.n_rows; ++i) {
     const uint32_t* kw = kws.data() + (size_t)i * nw;
-    const uint32_t h1 = h1s[(size_t)i], h2 = h2s[(size_t)i];
-    Mo.h_filt[(size_t)(h2 & (uint32_t)(fcap - 1))] |= filter_bits(filter_mix(h1, h2));
-    uint64_t slot = h1 & (uint64_t)(cap - 1);
+    const uint32_t ph = phs[(size_t)i], pl = pls[(size_t)i];
+    Mo.h_filt[(size_t)(pl & (uint32_t)(fcap - 1))] |= filter_pattern(filter_pattern_index(pl));
+    uint64_t slot = ph & (uint64_t)(cap - 1);
     int probe = 0;
     while (Mo.h_key[slot * nw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
     Mo.max_probe = std::max(Mo.max_probe, probe);
@@ -501,14 +506,15 @@ void build_hash(cvd_model& Mo) {
     slot_of[(size_t)i] = (int64_t)slot;
   }
   parallel_for(Mo.n_rows, [&](int64_t i, int) {
-    uint32_t* rw = Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw;
-    std::memcpy(rw, Mo.logp1.data() + (size_t)i * R, sizeof(double) * R);
+    uint32_t* dw = Mo.h_drow.data() + (size_t)i * Mo.h_rsw;
+    std::memcpy(dw, Mo.logp1.data() + (size_t)i * R, sizeof(double) * R);
     for (int r = 0; r < R; ++r) {
       const int64_t j = Mo.row_next[(size_t)i * R + r];
-      rw[2 * R + r] = (uint32_t)(j >= 0 ? (int32_t)slot_of[(size_t)j] : -1);
+      dw[2 * R + r] = (uint32_t)(j >= 0 ? (int32_t)j : -1);
     }
+    std::memcpy(Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw, dw, sizeof(uint32_t) * Mo.h_rsw);
   });
-  Mo.slot0 = (int32_t)slot_of[0];   // D_0 = 0 is row 0 in both model kinds
+  Mo.slot0 = 0;   // D_0 = 0 is row 0 in both model kinds
 }
 
 void build_bmk1(cvd_model& Mo, const Tabs& T) {

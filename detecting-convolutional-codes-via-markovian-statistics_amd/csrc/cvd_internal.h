@@ -32,12 +32,13 @@ struct cvd_model {
   int64_t hcap = 0;               // power of two, 0 = none
   int32_t max_probe = 0;
   std::vector<int64_t> row_next;  // [n_rows][2^n] row index of successor(row, r), -1 if not a row
-  std::vector<uint32_t> h_filt;   // [fcap] blocked Bloom filter words (filter_bits)
+  std::vector<uint32_t> h_filt;   // [fcap] blocked Bloom filter words (filter_pattern)
   int64_t fcap = 0;               // filter words, power of two
   std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector, word 0 = kEmptyKey if empty
   int32_t h_rsw = 0;              // row record stride in dwords (row_words)
-  std::vector<uint32_t> h_row;    // [hcap][h_rsw]: log P̂1[r] (2^n f64), successor slot[r] (2^n i32)
-  int32_t slot0 = 0;              // slot of D_0 = 0
+  std::vector<uint32_t> h_row;    // [hcap][h_rsw]: log P̂1[r] (2^n f64), successor row[r] (2^n i32, -1: none)
+  std::vector<uint32_t> h_drow;   // [n_rows][h_rsw]: the same records dense by row id (table mode)
+  int32_t slot0 = 0;              // row of D_0 = 0 (always 0)
   std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
   // k = 1 orbit kernel: successor(r ^ g0) = successor(r) with states 2j <-> 2j+1 swapped,
   // so only the representatives rep_0 < rep_1 < ... (r < r ^ g0) get an ACS.
@@ -62,6 +63,7 @@ struct cvd_model {
   uint32_t* d_filt = nullptr;
   uint32_t* d_hkey = nullptr;
   uint32_t* d_hrow = nullptr;
+  uint32_t* d_drow = nullptr;
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
   uint32_t* d_bfly = nullptr;

@@ -227,7 +227,7 @@ __device__ __forceinline__ uint32_t noise_word_wave(const GenArgs& a, uint32_t s
 template <int k, int n>
 __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   constexpr int SPW = 32 / n, NBITS = SPW * n;
-  constexpr uint32_t kValid = NBITS == 32 ? ~0u : (1u << NBITS) - 1u;
+  constexpr uint32_t kValid = NBITS == 32 ? ~0u : (1u << (NBITS % 32)) - 1u;
   static_assert(k >= 1 && k <= 2 && SPW * k <= 32, "gen_fast_kernel: shape");
   const int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (li >= a.count) return;
@@ -521,6 +521,7 @@ __global__ __launch_bounds__(kBlock) void detect_explicit_kernel(ExpArgs a) {
   using S = Shape<m, k, n>;
   __shared__ double s_lt[S::R + 1];
   if (threadIdx.x <= S::R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  fill_filter_patterns();
   __syncthreads();
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = q < a.nseq;
@@ -650,6 +651,7 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
   static_assert(m >= 2 && n == 2, "k1 orbit kernel shape");
   __shared__ double s_lt[R + 1];
   if (threadIdx.x <= R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  fill_filter_patterns();
   __syncthreads();
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = q < a.nseq;
@@ -983,7 +985,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   }
   if (nseq <= 0) return CVD_OK;
   ExpArgs a;
-  a.filt = M.d_filt; a.hkey = M.d_hkey; a.hrow = M.d_hrow; a.ltref = M.d_ltref;
+  a.filt = M.d_filt; a.hkey = M.d_hkey; a.hrow = M.d_hrow; a.drow = M.d_drow; a.ltref = M.d_ltref;
   a.bmp = bmp; a.slot0 = M.slot0;
   a.repmap = M.repmap; a.swmap = M.swmap; a.bfly_uni = M.bfly_uni;
   for (int w = 0; w < 4; ++w) a.bfly_even[w] = M.bfly_even[w];
@@ -1024,6 +1026,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_filt, M.h_filt))) return rc;
     if ((rc = dev_copy(M.d_hkey, M.h_key))) return rc;
     if ((rc = dev_copy(M.d_hrow, M.h_row))) return rc;
+    if ((rc = dev_copy(M.d_drow, M.h_drow))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
     if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
     if ((rc = dev_copy(M.d_bfly, M.bfly))) return rc;
@@ -1050,11 +1053,11 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_hkey, M.d_hrow, M.d_bmp, M.d_bmk1, M.d_bfly};
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_hkey, M.d_hrow, M.d_drow, M.d_bmp, M.d_bmk1, M.d_bfly};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
-  M.d_filt = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
+  M.d_filt = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
   M.d_bfly = nullptr;
   M.rtc_fn = nullptr;
   M.device = -1;

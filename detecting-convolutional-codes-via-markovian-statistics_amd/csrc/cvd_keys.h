@@ -25,7 +25,7 @@ CVD_HD unsigned key_swap(unsigned w) {
   const unsigned t = (w ^ (w >> 12)) & 0x0000F0F0u;
   return w ^ t ^ (t << 12);
 }
-CVD_HD int key_nibble(int M, int s) {   // nibble index of state s within its word
+constexpr CVD_HD int key_nibble(int M, int s) {   // nibble index of state s within its word
   const int b = s & 7;
   return M >= 8 ? (((b & 1) << 2) | (b & 2) | ((b >> 2) & 1)) : b;
 }
@@ -33,31 +33,41 @@ CVD_HD int key_nibble(int M, int s) {   // nibble index of state s within its wo
 CVD_HD unsigned rotl32(unsigned x, int r) { return (x << r) | (x >> (32 - r)); }
 CVD_HD unsigned long long mul_wide(unsigned a, unsigned b) { return (unsigned long long)a * b; }
 
-// 32-bit hash pair of a nibble-packed key (host and device must agree).  A
-// multiply-accumulate fold, one v_mad_u64_u32 per key word with a distinct odd
-// multiplier, then two 32x32->64 finalising products folded hi ^ lo; h1 picks
-// the home slot, h2 the filter word.  Quality only affects speed (probe
-// lengths, filter false positives), never results.
-CVD_HD void key_hash(const unsigned* w, int nw, unsigned& h1, unsigned& h2) {
+// Hash of a nibble-packed key (host and device must agree): a multiply-
+// accumulate fold, one v_mad_u64_u32 per key word with a distinct odd
+// multiplier, then one finalising 32x32->64 product p = x * C of the folded
+// word.  The home slot comes from p's high half (ph & hmask), the filter word
+// from the low bits of its low half (pl & fmask) and the filter pattern from
+// the top bits of pl (filter_pattern_index).  Quality
+// only affects speed (probe lengths, filter false positives), never results.
+CVD_HD void key_hash(const unsigned* w, int nw, unsigned& ph, unsigned& pl) {
   unsigned long long acc = 0x9E3779B97F4A7C15ull ^ (unsigned)nw;
   for (int i = 0; i < nw; ++i) acc += mul_wide(w[i], 0x85EBCA77u + 0x6A09E668u * (unsigned)i);
   const unsigned x = (unsigned)acc ^ (unsigned)(acc >> 32);
   const unsigned long long p = mul_wide(x, 0x85EBCA6Bu);
-  h1 = (unsigned)p ^ (unsigned)(p >> 32);
-  const unsigned long long q = mul_wide(x ^ (x >> 16), 0xC2B2AE35u);
-  h2 = (unsigned)q ^ (unsigned)(q >> 32);
+  ph = (unsigned)(p >> 32);
+  pl = (unsigned)p;
 }
 
 // Blocked Bloom filter over the row keys (explicit path): one 32-bit word per
-// key, three bits in it.  A lookup of a state that is not a row (most lookups
-// at p >= 0.05 and for every H2 sequence) ends on this one L2-resident load.
-// Word index from h2, bit positions from a third mix (kept as one register,
-// filter_bits(), until the word arrives; shift counts are the low 5 bits of
-// shifted copies, as v_lshlrev reads them).
-CVD_HD unsigned filter_mix(unsigned h1, unsigned h2) { return (h1 ^ rotl32(h2, 16)) * 0x9E3779B1u; }
-CVD_HD unsigned filter_bits(unsigned h3) {
-  return (1u << (h3 & 31u)) | (1u << ((h3 >> 5) & 31u)) | (1u << ((h3 >> 10) & 31u));
+// key, a pattern of three bits in it.  A lookup of a state that is not a row
+// (most lookups at p >= 0.05 and for every H2 sequence) ends on this one
+// L2-resident load.  The patterns come from a table of kFilterPatterns
+// three-bit words indexed by the top bits of pl (the device keeps it in LDS:
+// one LDS read instead of the shifts and ors of three bit positions).
+constexpr int kFilterPatBits = 10, kFilterPatterns = 1 << kFilterPatBits;
+CVD_HD unsigned filter_pattern(unsigned i) {
+  unsigned x = (i + 1u) * 0x9E3779B1u;
+  x ^= x >> 15;
+  x *= 0x85EBCA77u;
+  x ^= x >> 13;
+  const unsigned b0 = x & 31u;
+  unsigned b1 = (x >> 5) & 31u, b2 = (x >> 10) & 31u;
+  if (b1 == b0) b1 = (b1 + 1u) & 31u;
+  while (b2 == b0 || b2 == b1) b2 = (b2 + 1u) & 31u;
+  return (1u << b0) | (1u << b1) | (1u << b2);
 }
+CVD_HD unsigned filter_pattern_index(unsigned pl) { return pl >> (32 - kFilterPatBits); }
 
 // empty hash slot: key word 0 (a nibble-packed metric vector never has 15 in
 // every nibble, metrics stay <= (ceil(m/k)+1) n - 1 <= 14)
