@@ -477,7 +477,17 @@ void build_hash(cvd_model& Mo) {
     throw std::length_error("explicit-path row table over 4 GiB (too many learned rows)");
   Mo.hcap = cap;
   int64_t fcap = 64;
-  while (fcap * 2 < Mo.n_rows) fcap <<= 1;   // >= 16 filter bits per row
+  // >= 32 filter bits per row: a non-row passes the one-word filter ~0.25% of the
+  // time (~1% at 16 bits), and every false positive costs the wave the key and
+  // record loads and the key compare.  But at most 2 MiB: the filter must stay
+  // L2-resident beside the streams (4 MiB at p = 0.1, 8.2e5 rows, measured 9%
+  // slower per launch than 2 MiB, profiles/r02h/filter.jsonl).
+  // (CVD_FILTER_SCALE=s: filter words >= rows * 2^s, CVD_FILTER_MAX_LOG2: the
+  // cap, for timing studies)
+  int fscale = 0, fmax_log2 = 19;
+  if (const char* e = std::getenv("CVD_FILTER_SCALE")) fscale = std::max(-3, std::min(3, std::atoi(e)));
+  if (const char* e = std::getenv("CVD_FILTER_MAX_LOG2")) fmax_log2 = std::max(8, std::min(28, std::atoi(e)));
+  while ((fscale >= 0 ? fcap >> fscale : fcap << -fscale) < Mo.n_rows && fcap < ((int64_t)1 << fmax_log2)) fcap <<= 1;
   Mo.fcap = fcap;
   Mo.h_filt.assign((size_t)fcap, 0u);
   Mo.h_key.assign((size_t)cap * nw, kEmptyKey);

@@ -55,7 +55,7 @@ CVD_HD void key_hash(const unsigned* w, int nw, unsigned& ph, unsigned& pl) {
 // L2-resident load.  The patterns come from a table of kFilterPatterns
 // three-bit words indexed by the top bits of pl (the device keeps it in LDS:
 // one LDS read instead of the shifts and ors of three bit positions).
-constexpr int kFilterPatBits = 10, kFilterPatterns = 1 << kFilterPatBits;
+constexpr int kFilterPatBits = 12, kFilterPatterns = 1 << kFilterPatBits;
 CVD_HD unsigned filter_pattern(unsigned i) {
   unsigned x = (i + 1u) * 0x9E3779B1u;
   x ^= x >> 15;

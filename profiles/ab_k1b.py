@@ -10,6 +10,7 @@ rounds x variants detector launches are timed with HIP events on the launch
 stream, and every variant's per-trial sums must equal the first variant's.
 
 usage: python profiles/ab_k1b.py --variant= --variant=-DCVD_K1B_WAVES=5 --p 0.01 0.1
+       (host-side settings after a ';': --variant=";CVD_FILTER_SCALE=-1")
 prints one JSON line per p: per-variant launch times (ms), medians and mins.
 """
 import argparse
@@ -53,8 +54,15 @@ def main():
         det.generate(g2, N, p, a.seed, tag, 1, 2, B, out=r, q0=B, pitch=2 * B)
         models = []
         for v in a.variants:
-            os.environ["CVD_JIT_DEFINES"] = v
+            # a variant is JIT defines, optionally followed by ";VAR=value" host settings
+            defs, *envs = v.split(";")
+            os.environ["CVD_JIT_DEFINES"] = defs
+            for e in envs:
+                k_, v_ = e.split("=", 1)
+                os.environ[k_] = v_
             models.append(pkg.Model(det.dec, p, None, 200, 1.0, a.seed).upload(0))
+            for e in envs:
+                os.environ.pop(e.split("=", 1)[0], None)
         os.environ.pop("CVD_JIT_DEFINES", None)
         kernels = [pkg.KERNEL_NAMES[mod.info()["explicit_kernel"]] for mod in models]
         ref = None

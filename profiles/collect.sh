@@ -5,7 +5,7 @@
 #   bash profiles/collect.sh gpurun_out/prof "--cpu-baseline 0"
 set -euo pipefail
 OUT=${1:-gpurun_out/prof}
-ARGS=${2:-"--cpu-baseline 0"}
+ARGS=${2:-"--cpu-baseline 0 --early-decision 0"}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp

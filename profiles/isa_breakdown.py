@@ -45,11 +45,15 @@ def build_isa(cfg, defs, path):
 
 
 def main_loop(lines):
-    """Lines of the outermost loop (Depth=1) of the kernel body."""
-    hdr = next(i for i, l in enumerate(lines) if "=>This Loop Header: Depth=1" in l)
-    label = lines[hdr].split(":")[0]
-    back = max(i for i, l in enumerate(lines) if re.search(r"\bs_(c)?branch\w*\s+" + re.escape(label) + r"\b", l))
-    return lines[hdr:back + 1]
+    """Lines of the largest outermost loop (Depth=1) of the kernel body (the step
+    loop; the prologue's LDS table fill is a small loop of its own)."""
+    best = None
+    for hdr in (i for i, l in enumerate(lines) if "Loop Header: Depth=1" in l):
+        label = lines[hdr].split(":")[0]
+        backs = [i for i, l in enumerate(lines) if re.search(r"\bs_(c)?branch\w*\s+" + re.escape(label) + r"\b", l)]
+        if backs and (best is None or max(backs) - hdr > best[1] - best[0]):
+            best = (hdr, max(backs))
+    return lines[best[0]:best[1] + 1]
 
 
 def blocks(loop):
