@@ -46,7 +46,8 @@ P_GRID = [0.01, 0.02, 0.05, 0.10, 0.15, 0.20]
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
-VALU_PEAK_WINST = 1024 * 2.4e9 / 2
+SHADER_GHZ = 2.4
+VALU_PEAK_WINST = 1024 * SHADER_GHZ * 1e9 / 2
 
 # Informative grid points (Pd neither 0 nor 1) at each config's own N, found with the
 # C oracle (profiles/pd_points.jsonl): the headline sweep's Pd is 0 for m = 6 (the
@@ -334,10 +335,15 @@ def main():
             # per launch from the counter pass, over this run's live launch time
             winst = ipws * (2 * B / 64) * N
             ach = winst / (det_ms * 1e-3)
+            cpi = pmc.get("valu_cycles_per_inst")
             valu = {"insts_per_wave_step": ipws, "achieved": ach, "peak": VALU_PEAK_WINST,
                     "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WINST,
-                    "issue_cycle_weighted_frac": pmc.get("valu_issue_cycle_frac"),
-                    "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU) + live HIP-event time"}
+                    # the same instructions priced at their measured issue cost (VOP3/VOP3P ~4.2-4.5
+                    # cycles, VOP2 ~2.6, profiles/valu_issue_cycles.json) instead of 2 cycles each
+                    "cycles_per_inst": cpi,
+                    "issue_cycle_weighted_frac": (ach * cpi / (1024 * SHADER_GHZ * 1e9)) if cpi else None,
+                    "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU, opcode mix x "
+                              "profiles/valu_issue_cycles.json) + live HIP-event time"}
     c = counts.cpu().numpy()
     per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, (a.steps // len(p_grid) + (i < a.steps % len(p_grid))) * B * world),
                       "h1_successes": int(c[i, 0]), "h2_successes": int(c[i, 1])}

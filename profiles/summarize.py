@@ -85,6 +85,29 @@ def main(src, name):
         "batch": B,
         "N": N,
     }
+    # cycle-weighted VALU issue fraction: the step loop's opcode mix (static ISA of
+    # the kernel this tree builds, profiles/isa_breakdown.py) priced with the measured
+    # issue cost per class (profiles/valu_issue_cycles.json), times the dynamic
+    # instruction count, over the launch's SIMD-cycles
+    if out["detector"] == "markov" and "k1b" in out["kernel"]:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import isa_breakdown
+        import valu_model
+        import tempfile
+        with tempfile.TemporaryDirectory() as d:
+            lines = isa_breakdown.build_isa(out["config"], [], os.path.join(d, "k.s"))
+        mix = {}
+        for _name, ins in isa_breakdown.blocks(isa_breakdown.main_loop(lines)):
+            for x in ins:
+                if x.startswith("v_"):
+                    mix[x.split()[0]] = mix.get(x.split()[0], 0) + 0.25    # 4 steps per loop trip
+        cyc, by = valu_model.load_cycles()
+        avg, by_class = valu_model.weighted_cycles(mix, cyc)
+        out["valu_cycles_per_inst"] = avg
+        out["valu_cycles_source"] = ("static opcode mix of the step loop (profiles/isa_breakdown.py) x measured "
+                                     "issue cost per class (profiles/valu_issue_cycles.json)")
+        out["valu_mix_by_class_per_step"] = by_class
+        out["valu_issue_cycle_frac"] = per.get("SQ_INSTS_VALU", 0.0) * avg / (1024 * max(1.0, kernel_cycles))
     fn = f"pmc_{out['detector']}_{out['config']}.json"
     json.dump(out, open(os.path.join(ROOT, "profiles", fn), "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "counters_per_launch"}, indent=1))
