@@ -59,9 +59,8 @@ PD_POINTS = {
 }
 # The points were chosen on the first trial ids (0..2000) of seed 12345, so the check runs
 # on fresh ids: the CPU sample (and the GPU's exact repeat of it) starts at trial 10^6, the
-# large GPU sample at 2^40.  (Selection and confirmation data kept apart: the first ~800
-# trials of seed 12345 at the m6 point are a 3-4 sigma low outlier -- profiles/diag/ shows
-# it follows those streams, not the model, and that seeds 1-7 and 99 show no such deficit.)
+# large GPU sample at 2^40 (selection and confirmation data kept apart; round 1's streams
+# showed a 3-4 sigma low run in the first ~800 trials at the m6 point, profiles/diag/).
 PD_SAMPLE_START = 1_000_000
 # C0: demo_script.py preset 1 as BASELINE.json configs[0] states it -- (7,5) vs (5,7),
 # m = 2, N = 1e3, 1e3 trials, the demo's p grid and seed (demo_script.py:114-131)

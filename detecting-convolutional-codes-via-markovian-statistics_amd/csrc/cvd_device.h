@@ -142,7 +142,7 @@ struct ExpArgs {
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
   uint32_t bfly_uni;        // k = 1 butterfly kernel: every out(j, 0), j < 2^(m-1), in one class
   uint32_t bfly_even[4];    // k = 1 butterfly kernel: nibble masks of the butterflies with out(j, 0) in {00, 11}
-  uint32_t hmask, fmask;
+  uint32_t hmask, fmask, fmask4;   // fmask4 = fmask << 2 (filter byte offsets)
   int32_t max_probe;
   int32_t slot0;            // row of D_0 = 0
   double lp_unseen;
@@ -232,15 +232,24 @@ struct RowCursor {
   uint32_t pkey[NW];
   // record entries (log P̂1, successor row) of row s (dense records, table mode)
   // or of directory slot s (a hashed lookup's hit) for word rn
+  // (the successor entries' base moves into the uniform pointer, so each address is
+  // one shift-add of the lane's word onto the record offset)
+  // (the asm keeps LLVM from deriving one address from the other with two more ops)
+  __device__ static void rec_offsets(uint32_t off, uint32_t rn, uint32_t& o_lp, uint32_t& o_nx) {
+    asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(o_lp) : "v"(rn), "v"(off));
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(o_nx) : "v"(rn), "v"(off));
+  }
   __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
-    const uint32_t off = (uint32_t)s * RSB;
-    plp = ld_off<double>(a.drow, off + 8u * rn);
-    pnx = ld_off<int32_t>(a.drow, off + 4u * (2u * R + rn));
+    uint32_t o_lp, o_nx;
+    rec_offsets((uint32_t)s * RSB, rn, o_lp, o_nx);
+    plp = ld_off<double>(a.drow, o_lp);
+    pnx = ld_off<int32_t>(reinterpret_cast<const char*>(a.drow) + 8u * R, o_nx);
   }
   __device__ void prefetch_dir(const ExpArgs& a, int32_t s, uint32_t rn) {
-    const uint32_t off = (uint32_t)s * RSB;
-    plp = ld_off<double>(a.hrow, off + 8u * rn);
-    pnx = ld_off<int32_t>(a.hrow, off + 4u * (2u * R + rn));
+    uint32_t o_lp, o_nx;
+    rec_offsets((uint32_t)s * RSB, rn, o_lp, o_nx);
+    plp = ld_off<double>(a.hrow, o_lp);
+    pnx = ld_off<int32_t>(reinterpret_cast<const char*>(a.hrow) + 8u * R, o_nx);
   }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
     slot = a.slot0; hs = 0u; fb = 0u; fw = 0u; cand = false;
@@ -327,9 +336,12 @@ struct RowCursor {
       for (int w = 0; w < NW; ++w) key[w] = key_in[w] - kmu8;
       uint32_t ph, pl;
       key_hash(key, NW, ph, pl);
+      // byte offsets straight from the hash bits (cvd_keys.h: filter word (pl >> 2) & fmask,
+      // pattern (ph >> 2) & (kFilterPatterns - 1)): one AND each
       hs = ph & a.hmask;
-      fb = filter_patterns_lds()[cvd::filter_pattern_index(pl)];
-      fw = ld_off<uint32_t>(a.filt, (pl & a.fmask) * 4u);
+      fb = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(filter_patterns_lds()) +
+                                              (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 2)));
+      fw = ld_off<uint32_t>(a.filt, pl & a.fmask4);
     }
   }
 };

@@ -507,7 +507,7 @@ void build_hash(cvd_model& Mo) {
   for (int64_t i = 0; i < Mo.n_rows; ++i) {
     const uint32_t* kw = kws.data() + (size_t)i * nw;
     const uint32_t ph = phs[(size_t)i], pl = pls[(size_t)i];
-    Mo.h_filt[(size_t)(pl & (uint32_t)(fcap - 1))] |= filter_pattern(filter_pattern_index(pl));
+    Mo.h_filt[(size_t)filter_word_index(pl, (uint32_t)(fcap - 1))] |= filter_pattern(filter_pattern_index(ph));
     uint64_t slot = ph & (uint64_t)(cap - 1);
     int probe = 0;
     while (Mo.h_key[slot * nw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }

@@ -36,10 +36,11 @@ CVD_HD unsigned long long mul_wide(unsigned a, unsigned b) { return (unsigned lo
 // Hash of a nibble-packed key (host and device must agree): a multiply-
 // accumulate fold, one v_mad_u64_u32 per key word with a distinct odd
 // multiplier, then one finalising 32x32->64 product p = x * C of the folded
-// word.  The home slot comes from p's high half (ph & hmask), the filter word
-// from the low bits of its low half (pl & fmask) and the filter pattern from
-// the top bits of pl (filter_pattern_index).  Quality
-// only affects speed (probe lengths, filter false positives), never results.
+// word.  The home slot is ph & hmask, the filter word (pl >> 2) & fmask and the
+// filter pattern (ph >> 2) & (kFilterPatterns - 1) (the device takes both as
+// byte offsets, pl & (fmask << 2) and ph & ((kFilterPatterns - 1) << 2): one AND
+// each).  Quality only affects speed (probe lengths, filter false positives),
+// never results.
 CVD_HD void key_hash(const unsigned* w, int nw, unsigned& ph, unsigned& pl) {
   unsigned long long acc = 0x9E3779B97F4A7C15ull ^ (unsigned)nw;
   for (int i = 0; i < nw; ++i) acc += mul_wide(w[i], 0x85EBCA77u + 0x6A09E668u * (unsigned)i);
@@ -53,8 +54,8 @@ CVD_HD void key_hash(const unsigned* w, int nw, unsigned& ph, unsigned& pl) {
 // key, a pattern of three bits in it.  A lookup of a state that is not a row
 // (most lookups at p >= 0.05 and for every H2 sequence) ends on this one
 // L2-resident load.  The patterns come from a table of kFilterPatterns
-// three-bit words indexed by the top bits of pl (the device keeps it in LDS:
-// one LDS read instead of the shifts and ors of three bit positions).
+// three-bit words indexed by bits of ph (the device keeps it in LDS: one LDS
+// read instead of the shifts and ors of three bit positions).
 constexpr int kFilterPatBits = 12, kFilterPatterns = 1 << kFilterPatBits;
 CVD_HD unsigned filter_pattern(unsigned i) {
   unsigned x = (i + 1u) * 0x9E3779B1u;
@@ -67,7 +68,8 @@ CVD_HD unsigned filter_pattern(unsigned i) {
   while (b2 == b0 || b2 == b1) b2 = (b2 + 1u) & 31u;
   return (1u << b0) | (1u << b1) | (1u << b2);
 }
-CVD_HD unsigned filter_pattern_index(unsigned pl) { return pl >> (32 - kFilterPatBits); }
+CVD_HD unsigned filter_pattern_index(unsigned ph) { return (ph >> 2) & (unsigned)(kFilterPatterns - 1); }
+CVD_HD unsigned filter_word_index(unsigned pl, unsigned fmask) { return (pl >> 2) & fmask; }
 
 // empty hash slot: key word 0 (a nibble-packed metric vector never has 15 in
 // every nibble, metrics stay <= (ceil(m/k)+1) n - 1 <= 14)
