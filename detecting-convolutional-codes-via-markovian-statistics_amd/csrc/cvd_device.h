@@ -429,6 +429,34 @@ __device__ constexpr uint32_t e_sel(int j) {
   return xj == 0 ? 0x0100u : xj == 3 ? 0x0302u : xj == 1 ? 0x0504u : 0x0706u;
 }
 
+// Per received word y, the branch-metric registers of the specialised step in
+// LDS (filled at kernel start, read once per step instead of two popcounts,
+// two multiply-adds and the e-pair perms): [0] W0, [1] W1, [2 + 2c] / [3 + 2c]
+// the (e_j, e_{j+1}) / (2 - e_j, 2 - e_{j+1}) pairs of a butterfly pair whose
+// out(j, 0), out(j + 1, 0) classes are c & 3, c >> 2.
+constexpr int kWtabStride = 64;
+__device__ __forceinline__ uint32_t* wtab_lds() {
+  __shared__ uint32_t s_wt[4 * kWtabStride];
+  return s_wt;
+}
+template <uint64_t XM>
+__device__ constexpr int xm_class(int j) { return (int)((XM >> (2 * j)) & 3u); }
+__device__ __forceinline__ uint32_t wtab_entry(uint32_t y, int k) {
+  const uint32_t e0 = __builtin_popcount(y), e1 = __builtin_popcount(y ^ 1u);
+  const uint32_t W0 = e0 | ((2u - e0) << 16), W1 = e1 | ((2u - e1) << 16);
+  if (k == 0) return W0;
+  if (k == 1) return W1;
+  const int c = (k - 2) >> 1, x0 = c & 3, x1 = c >> 2;
+  const uint32_t s0 = x0 == 0 ? 0x0100u : x0 == 3 ? 0x0302u : x0 == 1 ? 0x0504u : 0x0706u;
+  const uint32_t s1 = x1 == 0 ? 0x0100u : x1 == 3 ? 0x0302u : x1 == 1 ? 0x0504u : 0x0706u;
+  return (k & 1) ? __builtin_amdgcn_perm(W1, W0, ((s1 ^ 0x0202u) << 16) | (s0 ^ 0x0202u))
+                 : __builtin_amdgcn_perm(W1, W0, (s1 << 16) | s0);
+}
+__device__ __forceinline__ void fill_wtab() {
+  uint32_t* t = wtab_lds();
+  for (int i = threadIdx.x; i < 4 * 34; i += blockDim.x) t[(i / 34) * kWtabStride + i % 34] = wtab_entry(i / 34, i % 34);
+}
+
 // The common step: D_t(y) for the lane's own word, in place in Dp (pair i is
 // dead once butterflies 2i, 2i + 1 and 2i - H, 2i + 1 - H have read it), and
 // the nibble keys of the raw metrics minus the running offset.
@@ -456,10 +484,11 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
   // (e, 2 - e) for out(j, 0) = 0 and 1; out 3 and 2 are their swaps (op_sel),
   // so no table and no v_perm per butterfly
   uint32_t W0 = 0u, W1 = 0u;
+  const uint32_t* wt = nullptr;   // this word's row of the LDS table (wtab_entry)
   if constexpr (kSpec) {
-    const uint32_t e0 = __builtin_popcount(rr), e1 = __builtin_popcount(rr ^ 1u);
-    W0 = e0 | ((2u - e0) << 16);
-    W1 = e1 | ((2u - e1) << 16);
+    wt = wtab_lds() + rr * kWtabStride;
+    W0 = wt[0];
+    W1 = wt[1];
   }
   auto pack = [&](int w, uint32_t sel_pk) {
     // word w = states 8w..8w+7 in nibble order bitrev3 (device key layout):
@@ -481,8 +510,8 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
       const uint32_t ra = Dp[j >> 1], rb = Dp[(j >> 1) + H / 2];
       // (e_j, e_{j+1}) and (2 - e_j, 2 - e_{j+1}) (compile-time selectors; the
       // compiler shares equal ones across butterfly pairs)
-      const uint32_t ep = __builtin_amdgcn_perm(W1, W0, (e_sel<XM>(j + 1) << 16) | e_sel<XM>(j));
-      const uint32_t cp = __builtin_amdgcn_perm(W1, W0, ((e_sel<XM>(j + 1) ^ 0x0202u) << 16) | (e_sel<XM>(j) ^ 0x0202u));
+      const int c = xm_class<XM>(j) | (xm_class<XM>(j + 1) << 2);   // compile-time after unrolling
+      const uint32_t ep = wt[2 + 2 * c], cp = wt[3 + 2 * c];
       E[j] = as_u32(__builtin_elementwise_min(as_us2(ra + ep), as_us2(rb + cp)));       // (D'(2j), D'(2j+2))
       E[j + 1] = as_u32(__builtin_elementwise_min(as_us2(ra + cp), as_us2(rb + ep)));   // (D'(2j+1), D'(2j+3))
       if ((j & 3) == 2) pack(j >> 2, 0x06040200u);
@@ -543,6 +572,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
   __shared__ double s_lt[R + 1];
   if (threadIdx.x <= R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
   fill_filter_patterns();
+  if constexpr (kSpec) fill_wtab();
   __syncthreads();
   // Sequence index without a VGPR live across the step loop: the wave's first
   // index in SGPRs, the lane from mbcnt, recomputed after the loop; validity
