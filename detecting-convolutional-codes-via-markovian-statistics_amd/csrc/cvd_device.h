@@ -331,11 +331,8 @@ struct RowCursor {
     if (slot >= 0) {
       prefetch_row(a, slot, rn);
     } else if (slot == -2 && !(CVD_ABL & 4)) {
-      uint32_t key[NW];
-#pragma unroll
-      for (int w = 0; w < NW; ++w) key[w] = key_in[w] - kmu8;
       uint32_t ph, pl;
-      key_hash(key, NW, ph, pl);
+      cvd::key_hash_less(key_in, NW, kmu8 & 1u, ph, pl);   // = key_hash(key_in - kmu8)
       // byte offsets straight from the hash bits (cvd_keys.h: filter word (pl >> 2) & fmask,
       // pattern (ph >> 2) & (kFilterPatterns - 1)): one AND each
       hs = ph & a.hmask;
@@ -395,7 +392,7 @@ __device__ __forceinline__ void k1b_trace(uint8_t* tr, int64_t t, int64_t nseq, 
 #define CVD_K1B_MID 2
 #endif
 #ifndef CVD_K1B_LAZYKEY
-#define CVD_K1B_LAZYKEY 0
+#define CVD_K1B_LAZYKEY 1
 #endif
 constexpr int kK1bWavesPerSimd = CVD_K1B_WAVES;
 constexpr int kRenorm = 128;   // O <= 128: raw pair values stay < 256 (byte packing)

@@ -50,6 +50,26 @@ CVD_HD void key_hash(const unsigned* w, int nw, unsigned& ph, unsigned& pl) {
   pl = (unsigned)p;
 }
 
+// key_hash of the key whose every nibble is one less (mu = 1) or equal (mu = 0)
+// to w's: the fold is linear in the words, and w_i - mu * 0x11111111 never
+// borrows (every nibble of w is >= mu), so the accumulator is the plain fold of
+// w minus mu * K_nw, K_nw = sum_i 0x11111111 * multiplier_i (mod 2^64) -- one
+// select of the start value instead of a subtraction per key word.
+CVD_HD unsigned long long key_fold_offset(int nw) {
+  unsigned long long k = 0;
+  for (int i = 0; i < nw; ++i) k += mul_wide(0x11111111u, 0x85EBCA77u + 0x6A09E668u * (unsigned)i);
+  return k;
+}
+CVD_HD void key_hash_less(const unsigned* w, int nw, unsigned mu, unsigned& ph, unsigned& pl) {
+  const unsigned long long a0 = 0x9E3779B97F4A7C15ull ^ (unsigned)nw;
+  unsigned long long acc = mu ? a0 - key_fold_offset(nw) : a0;
+  for (int i = 0; i < nw; ++i) acc += mul_wide(w[i], 0x85EBCA77u + 0x6A09E668u * (unsigned)i);
+  const unsigned x = (unsigned)acc ^ (unsigned)(acc >> 32);
+  const unsigned long long p = mul_wide(x, 0x85EBCA6Bu);
+  ph = (unsigned)(p >> 32);
+  pl = (unsigned)p;
+}
+
 // Blocked Bloom filter over the row keys (explicit path): one 32-bit word per
 // key, a pattern of three bits in it.  A lookup of a state that is not a row
 // (most lookups at p >= 0.05 and for every H2 sequence) ends on this one

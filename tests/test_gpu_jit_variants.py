@@ -1,0 +1,43 @@
+"""Build-time variants of the code-specialised m = 6 detector kernel (CVD_JIT_DEFINES,
+csrc/cvd_rtc.cpp) must give per-trial fp64 sums bit-identical to the default kernel
+and to the C oracle: the eager key normalisation (CVD_K1B_LAZYKEY=0; the default
+keeps the key offset by the step minimum and folds the offset into the hash), and the
+lookup-load placement knob."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import c_oracle as C
+
+pytestmark = pytest.mark.gpu
+SEED = 12345
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda", 0)
+
+
+def _sums(pkg, det, cc, p, N, T, t0, defines, monkeypatch):
+    monkeypatch.setenv("CVD_JIT_DEFINES", defines)
+    model = pkg.Model(det.dec, p, None, 200, 1.0, SEED).upload(0)
+    monkeypatch.delenv("CVD_JIT_DEFINES")
+    assert model.jit_status()[0] == 1, model.jit_status()
+    return det.run_trials(model, cc["gen1"], cc["gen2"], N, p, SEED, t0, t0 + T, return_sums=True)["sums"]
+
+
+@pytest.mark.parametrize("p", [0.01, 0.1])
+def test_lazy_key_variants_bit_identical(pkg, dev, p, monkeypatch):
+    cc = pkg.CONFIG_CODES["m6"]
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    N, T, t0 = 20_000, 2048, 777
+    ref = _sums(pkg, det, cc, p, N, T, t0, "", monkeypatch)
+    for v in ("-DCVD_K1B_LAZYKEY=0", "-DCVD_K1B_LAZYKEY=1", "-DCVD_K1B_MID=1"):
+        got = _sums(pkg, det, cc, p, N, T, t0, v, monkeypatch)
+        assert np.array_equal(got, ref), v
+    # and the C oracle (independent restatement of the sparse-model policy) on a few trials
+    c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
+    cm = C.Model(c1, p, None, 200, 1.0, SEED)
+    _, s_cpu = cm.run_trials(c1, c2, N, p, SEED, t0, t0 + 16, sums=True)
+    assert np.array_equal(ref[:16], s_cpu)
