@@ -262,12 +262,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=det.device, dtype=torch.float64)
-        if a.dist_backend == "gloo":
-            t = t.cpu()
+    def max_over_ranks(x):
+        # RCCL reduces device tensors only; gloo host tensors
+        t = torch.tensor([x], device=det.device if a.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return float(t.item())
+
+    if dist:
+        elapsed = max_over_ranks(elapsed)
     gen_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     det_each = [e[2].elapsed_time(e[3]) for e in events]
     det_ms = float(np.mean(det_each))
@@ -292,9 +294,7 @@ def main():
         torch.cuda.synchronize()
         el2 = time.perf_counter() - t1
         if dist:
-            t = torch.tensor([el2], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el2 = float(t.item())
+            el2 = max_over_ranks(el2)
         early[0] = False
         d2 = [e[2].elapsed_time(e[3]) for e in ev2]
         early_out = {"value": a.steps * B * world / el2, "unit": "trials/s", "ms_per_step": el2 / a.steps * 1e3,
