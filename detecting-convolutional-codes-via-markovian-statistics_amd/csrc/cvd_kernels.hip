@@ -474,76 +474,6 @@ __global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
 
-// Enumerated automaton, small models (S * 2^n <= 5120: m = 2, m = 3): one 32-byte
-// LDS slot per (state, word) holding {log P̂1, log T_ref (the count already
-// resolved), byte offset of the next state's slots}.  Per step: one bit-field
-// extract and one shift-add for the slot address, one 16-byte and one 4-byte LDS
-// read, two fp64 adds -- against ~10 VALU for the 16-bit record form, which has to
-// split the record and index two more tables.
-template <int n>
-__device__ __forceinline__ void slot_step(uint32_t sym, uint32_t& st, double& lp, double& lr, const char* smem) {
-  const uint32_t off = st + (sym << 5);
-  const double2 v = *reinterpret_cast<const double2*>(smem + off);
-  st = *reinterpret_cast<const uint32_t*>(smem + off + 16);
-  lp += v.x;                         // log P̂1[i, j]   (Pd_plotter.py:213)
-  lr += v.y;                         // log T_ref[i, j] = log(c / 2^n) (Pd_plotter.py:214)
-}
-
-template <int n, int BS>
-__global__ __launch_bounds__(BS) void detect_slot_kernel(TabArgs a) {
-  constexpr int R = 1 << n, SPW = 32 / n;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int SR = (int)a.S * R;
-  for (int i = threadIdx.x; i < SR; i += BS) {
-    const uint32_t e = a.rec[i];
-    double* d = reinterpret_cast<double*>(smem + (size_t)i * 32);
-    d[0] = a.logp1[i];
-    d[1] = a.ltref[e & 15u];
-    reinterpret_cast<uint32_t*>(smem + (size_t)i * 32)[4] = (e >> 4) * (uint32_t)(R * 32);
-  }
-  __syncthreads();
-  const int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x;
-  const bool valid = q < a.nseq;
-  double lp = 0.0, lr = 0.0;
-  if (valid) {
-    const int64_t N = a.N, nwords = (N + SPW - 1) / SPW, nchunks = (nwords + 3) / 4;
-    const int64_t full = N / (4 * SPW);           // chunks whose 4 words are all full
-    const uint4* rc = reinterpret_cast<const uint4*>(a.r) + q;
-    const int64_t cs = a.nseq;                    // uint4 stride between chunks of one sequence
-    uint4 cur = make_uint4(0u, 0u, 0u, 0u), nxt = cur;
-    if (nchunks > 0) cur = rc[0];
-    if (nchunks > 1) nxt = rc[cs];
-    uint32_t st = 0;                              // slots of D_0 = 0 (first BFS state)
-    int dec = 0;                                  // early decision (0 = open)
-    for (int64_t c = 0; c < nchunks; ++c) {
-      if (a.early && c > 0 && (c & 1) == 0 && c <= full) {   // every 2 chunks (8 words)
-        if (!dec) dec = early_decide(lp, lr, N - c * 4 * SPW, a.lt_min, a.lp_min);
-        if (__ballot(dec == 0) == 0) break;
-      }
-      const uint4 ch = cur;
-      cur = nxt;
-      if (c + 2 < nchunks) nxt = rc[(c + 2) * cs];
-      const uint32_t wv[4] = {ch.x, ch.y, ch.z, ch.w};
-      if (c < full) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int i = 0; i < SPW; ++i) slot_step<n>((wv[e] >> (n * i)) & (uint32_t)(R - 1), st, lp, lr, smem);
-      } else {
-        for (int e = 0; e < 4; ++e) {
-          const int64_t t0 = (4 * c + e) * SPW;
-          if (t0 >= N) break;
-          const int ns = (int)min((int64_t)SPW, N - t0);
-          for (int i = 0; i < ns; ++i) slot_step<n>((wv[e] >> (n * i)) & (uint32_t)(R - 1), st, lp, lr, smem);
-        }
-      }
-    }
-    if (a.sums) { a.sums[2 * q] = lp; a.sums[2 * q + 1] = lr; }
-    early_final(dec, lp, lr);
-  }
-  count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
-}
-
 // pk16 minimum over L registers as a log-depth tree (independent ops issue back to back)
 template <int L>
 __device__ __forceinline__ us2 tree_min(const uint32_t (&A)[L]) {
@@ -998,19 +928,6 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
   // LDS-resident compact model (16-bit records): 1024-thread blocks when it
   // takes most of a CU's 160 KiB, else 256-thread blocks
-  const size_t lds32 = (size_t)M.S * R * 32;
-  if (lds32 <= 160 * 1024 && (M.dec.n == 2 || M.dec.n == 3) && !std::getenv("CVD_TABLE_WIDE") &&
-      !std::getenv("CVD_TABLE16")) {
-    const bool big = lds32 > 40 * 1024;
-    const int bs = big ? 1024 : kBlock;
-    void (*kern)(TabArgs) = M.dec.n == 2 ? (big ? detect_slot_kernel<2, 1024> : detect_slot_kernel<2, kBlock>)
-                                         : (big ? detect_slot_kernel<3, 1024> : detect_slot_kernel<3, kBlock>);
-    if (lds32 > 64 * 1024)
-      HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds32));
-    hipLaunchKernelGGL(kern, dim3((unsigned)((nseq + bs - 1) / bs)), dim3(bs), lds32, (hipStream_t)stream, a);
-    HIP_CHECK(hipGetLastError());
-    return CVD_OK;
-  }
   const size_t lds16 = (size_t)M.S * R * (sizeof(double) + sizeof(uint16_t)) + (R + 1) * sizeof(double);
   if (M.S < 4096 && lds16 <= 160 * 1024 && (M.dec.n == 2 || M.dec.n == 3) && !std::getenv("CVD_TABLE_WIDE")) {
     const bool big = lds16 > 40 * 1024;
