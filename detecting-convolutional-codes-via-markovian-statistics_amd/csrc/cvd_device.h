@@ -326,13 +326,15 @@ struct RowCursor {
     return lpv;
   }
   // D_t's key is known: issue the next step's loads
+  // kmu8: the key's offset c * 0x11111111, c in {kLo, kLo + 1}
+  template <int kLo = 0>
   __device__ void prefetch(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t rn, uint32_t kmu8 = 0u) {
     if (CVD_ABL & 1) return;
     if (slot >= 0) {
       prefetch_row(a, slot, rn);
     } else if (slot == -2 && !(CVD_ABL & 4)) {
       uint32_t ph, pl;
-      cvd::key_hash_less(key_in, NW, kmu8 & 1u, ph, pl);   // = key_hash(key_in - kmu8)
+      cvd::key_hash_less<kLo>(key_in, NW, kmu8 & 3u, ph, pl);   // = key_hash(key_in - kmu8)
       // byte offsets straight from the hash bits (cvd_keys.h: filter word (pl >> 2) & fmask,
       // pattern (ph >> 2) & (kFilterPatterns - 1)): one AND each
       hs = ph & a.hmask;
@@ -433,25 +435,36 @@ __device__ constexpr uint32_t e_sel(int j) {
 // out(j, 0), out(j + 1, 0) classes are c & 3, c >> 2.
 constexpr int kWtabStride = 64;
 __device__ __forceinline__ uint32_t* wtab_lds() {
-  __shared__ uint32_t s_wt[4 * kWtabStride];
+  __shared__ uint32_t s_wt[8 * kWtabStride];
   return s_wt;
 }
 template <uint64_t XM>
 __device__ constexpr int xm_class(int j) { return (int)((XM >> (2 * j)) & 3u); }
-__device__ __forceinline__ uint32_t wtab_entry(uint32_t y, int k) {
+// Row y + 4 mu holds the metrics minus the previous step's minimum mu (the
+// specialised step keeps the pairs at D + 1 + mu, see k1b_body): W0 / W1 as
+// 16-bit lanes (e - mu may be -1 = 0xFFFF: the packed adds wrap per lane), the
+// e-pairs as the 32-bit integer lo + 65536 hi (the plain 32-bit adds of the
+// no-broadcast step then give the lane sums, all >= 0, without a borrow
+// crossing lanes).
+__device__ __forceinline__ uint32_t wtab_entry(uint32_t y, uint32_t mu, int k) {
   const uint32_t e0 = __builtin_popcount(y), e1 = __builtin_popcount(y ^ 1u);
   const uint32_t W0 = e0 | ((2u - e0) << 16), W1 = e1 | ((2u - e1) << 16);
-  if (k == 0) return W0;
-  if (k == 1) return W1;
+  const uint32_t mm = mu * 0x10001u;
+  if (k == 0) return as_u32(as_us2(W0) - as_us2(mm));
+  if (k == 1) return as_u32(as_us2(W1) - as_us2(mm));
   const int c = (k - 2) >> 1, x0 = c & 3, x1 = c >> 2;
   const uint32_t s0 = x0 == 0 ? 0x0100u : x0 == 3 ? 0x0302u : x0 == 1 ? 0x0504u : 0x0706u;
   const uint32_t s1 = x1 == 0 ? 0x0100u : x1 == 3 ? 0x0302u : x1 == 1 ? 0x0504u : 0x0706u;
-  return (k & 1) ? __builtin_amdgcn_perm(W1, W0, ((s1 ^ 0x0202u) << 16) | (s0 ^ 0x0202u))
-                 : __builtin_amdgcn_perm(W1, W0, (s1 << 16) | s0);
+  const uint32_t pr = (k & 1) ? __builtin_amdgcn_perm(W1, W0, ((s1 ^ 0x0202u) << 16) | (s0 ^ 0x0202u))
+                              : __builtin_amdgcn_perm(W1, W0, (s1 << 16) | s0);
+  return pr - mm;   // (lo - mu) + 65536 (hi - mu) as a 32-bit integer
 }
 __device__ __forceinline__ void fill_wtab() {
   uint32_t* t = wtab_lds();
-  for (int i = threadIdx.x; i < 4 * 34; i += blockDim.x) t[(i / 34) * kWtabStride + i % 34] = wtab_entry(i / 34, i % 34);
+  for (int i = threadIdx.x; i < 8 * 34; i += blockDim.x) {
+    const int row = i / 34, k = i % 34;
+    t[row * kWtabStride + k] = wtab_entry((uint32_t)(row & 3), (uint32_t)(row >> 2), k);
+  }
 }
 
 // The common step: D_t(y) for the lane's own word, in place in Dp (pair i is
@@ -472,7 +485,7 @@ __device__ __forceinline__ void fill_wtab() {
 template <int m, bool kSpec, uint64_t XM, int kKind = 0>
 __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1 << m) / 8, 4>& cur, uint32_t rr,
                                         uint32_t (&Dp)[(1 << m) / 2], uint32_t (&kw)[(1 << m) / 8],
-                                        uint32_t sel, uint32_t O8, uint32_t& zn) {
+                                        uint32_t sel, uint32_t O8, uint32_t& zn, uint32_t mu_prev = 0u) {
   constexpr int M = 1 << m, H = M / 2;
   constexpr int LIN = kKind == 2 ? 1 : 0;
   constexpr int kMid = ((H * CVD_K1B_MID) / 4) & ~1;   // even: both loops reach it
@@ -483,7 +496,7 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
   uint32_t W0 = 0u, W1 = 0u;
   const uint32_t* wt = nullptr;   // this word's row of the LDS table (wtab_entry)
   if constexpr (kSpec) {
-    wt = wtab_lds() + rr * kWtabStride;
+    wt = wtab_lds() + (rr + 4u * mu_prev) * kWtabStride;
     W0 = wt[0];
     W1 = wt[1];
   }
@@ -492,8 +505,11 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
     // bytes (s0, s2, s1, s3) and (s4, s6, s5, s7) by one v_perm each (metrics + O < 256)
     const uint32_t x = __builtin_amdgcn_perm(E[4 * w + 1], E[4 * w], sel_pk);
     const uint32_t y = __builtin_amdgcn_perm(E[4 * w + 3], E[4 * w + 2], sel_pk);
-    const uint32_t v = x + (y << 4) - O8;             // nibbles = raw metric - offset <= 14
-    zn |= (v - 0x11111111u) & ~v;
+    // table-driven kernel: nibbles = raw metric - offset (0..14), a zero nibble is
+    // the step minimum 0; specialised: the pairs already are D + 1 + mu (1..15) and
+    // a nibble < 2 (hasless(v, 2): existence is exact) is the step minimum 0
+    const uint32_t v = kSpec ? x + (y << 4) : x + (y << 4) - O8;
+    zn |= (v - (kSpec ? 0x22222222u : 0x11111111u)) & ~v;
     kw[w] = v;
   };
   if constexpr (kKind == 1) {
@@ -580,14 +596,21 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
   const uint64_t vmask = __ballot(valid), hmask = __ballot(q < a.n_h1);
   double lp = 0.0, lr = 0.0;
   if (valid) {
-    uint32_t Dp[H];   // (D(2i), D(2i+1)) + O, packed 16-bit
+    // Pairs (D(2i), D(2i+1)), packed 16-bit.  Table-driven kernel: D + O, O the
+    // sum of the step minima since the last renormalisation (every kRenorm
+    // steps).  Specialised kernel: D + 1 + mu, mu the last step minimum (0 or 1),
+    // kept there by taking mu off the next step's branch metrics (the LDS table
+    // row y + 4 mu): the nibble keys need no offset subtraction and nothing is
+    // renormalised.
+    uint32_t Dp[H];
 #pragma unroll
-    for (int i = 0; i < H; ++i) Dp[i] = 0u;
-    uint32_t key[NW];  // normalised D_{t-1}, device key layout
+    for (int i = 0; i < H; ++i) Dp[i] = kSpec ? 0x00010001u : 0u;
+    uint32_t key[NW];  // D_{t-1}, device key layout (+ kmu8 in every nibble)
 #pragma unroll
-    for (int w = 0; w < NW; ++w) key[w] = 0u;
-    uint32_t O = 0u, O8 = 0u;   // O8 = O * 0x11111111
-    uint32_t kmu8 = 0u;         // nibble offset of the stored key (lazy normalisation)
+    for (int w = 0; w < NW; ++w) key[w] = kSpec && CVD_K1B_LAZYKEY ? 0x11111111u : 0u;
+    uint32_t O = 0u, O8 = 0u;   // O8 = O * 0x11111111 (table-driven kernel)
+    uint32_t mu_prev = 0u;      // step minimum of D_{t-1} (specialised kernel)
+    uint32_t kmu8 = kSpec && CVD_K1B_LAZYKEY ? 0x11111111u : 0u;   // nibble offset of the stored key
     if constexpr (kTrace) k1b_trace<m>(a.trace, 0, a.nseq, qwave + lane_id(), key);
     // Received words: word w of this sequence at rbase + (w/4)*cstride + w%4
     // (16-byte chunks, include/cvd.h).  Only the current word and the next are
@@ -615,12 +638,17 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       asm volatile("" : "+s"(tb));   // per step: the table is re-read (scalar cache), not held in SGPRs
       uint32_t kw[NW];
       uint32_t zn = 0u;
-      k1b_acs<m, kSpec, XM, KIND>(a, tb, cur, rr, Dp, kw, sel, O8, zn);
+      k1b_acs<m, kSpec, XM, KIND>(a, tb, cur, rr, Dp, kw, sel, O8, zn, mu_prev);
       // Eq. 5: step minimum 0 or 1
       const uint32_t mu = (zn & 0x88888888u) == 0u;
-      const uint32_t mu8 = mu ? 0x11111111u : 0u;
-      O += mu;
-      O8 += mu8;
+      // offset of kw's nibbles over the normalised D_t
+      const uint32_t off8 = kSpec ? (mu ? 0x22222222u : 0x11111111u) : (mu ? 0x11111111u : 0u);
+      if constexpr (kSpec) {
+        mu_prev = mu;
+      } else {
+        O += mu;
+        O8 += mu ? 0x11111111u : 0u;
+      }
       // P̂1 row of D_{t-1}
       cur.fence(zn);                          // zn depends on the whole ACS
       cur.template fence_keys<NW>(zn);
@@ -645,12 +673,12 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
         if (!kUniKnown || kUni) hx |= dh[v];
         sym |= dh[v] & ((kSpec ? xm_even<m, XM>(v) : a.bfly_even[v]) ^ pm);
       }
-      // D_t's key.  Lazy form: raw nibbles (canonical + mu in every nibble, no
-      // borrow since mu = 1 means every nibble >= 1); the halves test only asks
+      // D_t's key.  Lazy form: raw nibbles (canonical + off8 in every nibble, no
+      // borrow since every nibble is >= its offset); the halves test only asks
       // which nibbles are equal, which the common offset leaves unchanged
 #pragma unroll
-      for (int v = 0; v < NW; ++v) key[v] = CVD_K1B_LAZYKEY ? kw[v] : kw[v] - mu8;
-      kmu8 = CVD_K1B_LAZYKEY ? mu8 : 0u;
+      for (int v = 0; v < NW; ++v) key[v] = CVD_K1B_LAZYKEY ? kw[v] : kw[v] - off8;
+      kmu8 = CVD_K1B_LAZYKEY ? off8 : 0u;
       // y ^ 3: D_t is the pair swap of D_t(y); y ^ 1, y ^ 2: equal iff halves and uni
       const bool uni = kUniKnown ? kUni : a.bfly_uni != 0u;
       const uint32_t c = (CVD_ABL & 2) ? 1u : 1u + (sym == 0u) + ((uni && hx == 0u) ? 2u : 0u);
@@ -661,7 +689,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
         for (int v = 0; v < NW; ++v) ck[v] = key[v] - kmu8;
         k1b_trace<m>(a.trace, t, a.nseq, qwave + lane_id(), ck);
       }
-      cur.prefetch(a, key, rn, kmu8);
+      cur.template prefetch<kSpec && CVD_K1B_LAZYKEY ? 1 : 0>(a, key, rn, kmu8);
     };
 
     // groups of 4 steps (a quarter word): the 10 bits they read (4 words and
@@ -683,11 +711,13 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
         nw = load_word(w + 1);
       }
       if (((t + 4) & (kRenorm - 1)) == 0) {
-        const us2 o2 = as_us2(O * 0x10001u);
+        if constexpr (!kSpec) {
+          const us2 o2 = as_us2(O * 0x10001u);
 #pragma unroll
-        for (int i = 0; i < H; ++i) Dp[i] = as_u32(as_us2(Dp[i]) - o2);
-        O = 0u;
-        O8 = 0u;
+          for (int i = 0; i < H; ++i) Dp[i] = as_u32(as_us2(Dp[i]) - o2);
+          O = 0u;
+          O8 = 0u;
+        }
         static_assert(kRenorm == kEarlyEvery, "early checks ride on the renormalisation");
         if (a.early) {
           if (!dec) dec = early_decide(lp, lr, N - (t + 4), a.lt_min, a.lp_min);

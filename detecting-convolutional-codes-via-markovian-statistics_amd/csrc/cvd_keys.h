@@ -50,19 +50,23 @@ CVD_HD void key_hash(const unsigned* w, int nw, unsigned& ph, unsigned& pl) {
   pl = (unsigned)p;
 }
 
-// key_hash of the key whose every nibble is one less (mu = 1) or equal (mu = 0)
-// to w's: the fold is linear in the words, and w_i - mu * 0x11111111 never
-// borrows (every nibble of w is >= mu), so the accumulator is the plain fold of
-// w minus mu * K_nw, K_nw = sum_i 0x11111111 * multiplier_i (mod 2^64) -- one
-// select of the start value instead of a subtraction per key word.
+// key_hash of the key whose every nibble is c less than w's (c = 0..3): the fold
+// is linear in the words, and w_i - c * 0x11111111 never borrows (every nibble
+// of w is >= c), so the accumulator is the plain fold of w minus c * K_nw,
+// K_nw = sum_i 0x11111111 * multiplier_i (mod 2^64) -- a select of the start
+// value instead of a subtraction per key word.
 CVD_HD unsigned long long key_fold_offset(int nw) {
   unsigned long long k = 0;
   for (int i = 0; i < nw; ++i) k += mul_wide(0x11111111u, 0x85EBCA77u + 0x6A09E668u * (unsigned)i);
   return k;
 }
-CVD_HD void key_hash_less(const unsigned* w, int nw, unsigned mu, unsigned& ph, unsigned& pl) {
-  const unsigned long long a0 = 0x9E3779B97F4A7C15ull ^ (unsigned)nw;
-  unsigned long long acc = mu ? a0 - key_fold_offset(nw) : a0;
+CVD_HD unsigned long long key_fold_start(int nw, unsigned c) {
+  return (0x9E3779B97F4A7C15ull ^ (unsigned)nw) - (unsigned long long)c * key_fold_offset(nw);
+}
+// kLo: the offset is kLo or kLo + 1 (two constants, one select)
+template <int kLo>
+CVD_HD void key_hash_less(const unsigned* w, int nw, unsigned c, unsigned& ph, unsigned& pl) {
+  unsigned long long acc = c == (unsigned)kLo + 1u ? key_fold_start(nw, kLo + 1) : key_fold_start(nw, kLo);
   for (int i = 0; i < nw; ++i) acc += mul_wide(w[i], 0x85EBCA77u + 0x6A09E668u * (unsigned)i);
   const unsigned x = (unsigned)acc ^ (unsigned)(acc >> 32);
   const unsigned long long p = mul_wide(x, 0x85EBCA6Bu);
