@@ -187,6 +187,38 @@ __device__ __forceinline__ void noise_plane_m(uint32_t r, uint32_t pm, uint32_t&
   U &= ~(r ^ pm);
 }
 
+// Four planes against thr's four bits B (most significant first, compile time):
+// the planes' 4-bit value R of each code bit is below B (flip), equal (still
+// undecided) or above (no flip) -- two boolean functions of four inputs that the
+// compiler reduces to a few v_bitop3, instead of three operations per plane.
+template <int B>
+__device__ __forceinline__ void noise_planes4(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& U,
+                                              uint32_t& F) {
+  const uint32_t r[4] = {r0, r1, r2, r3};
+  uint32_t e = ~0u, l = 0u;   // equal so far / already below
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if ((B >> (3 - i)) & 1) {
+      l |= e & ~r[i];
+      e &= r[i];
+    } else {
+      e &= ~r[i];
+    }
+  }
+  F |= U & l;
+  U &= e;
+}
+// thr's 4-bit group `nib` (wave-uniform) picks the specialised form
+__device__ __forceinline__ void noise_planes4_rt(uint32_t nib, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
+                                                 uint32_t& U, uint32_t& F) {
+  switch (__builtin_amdgcn_readfirstlane(nib) & 15u) {
+#define CVD_P4(b) case b: noise_planes4<b>(r0, r1, r2, r3, U, F); break;
+    CVD_P4(0) CVD_P4(1) CVD_P4(2) CVD_P4(3) CVD_P4(4) CVD_P4(5) CVD_P4(6) CVD_P4(7)
+    CVD_P4(8) CVD_P4(9) CVD_P4(10) CVD_P4(11) CVD_P4(12) CVD_P4(13) CVD_P4(14) CVD_P4(15)
+#undef CVD_P4
+  }
+}
+
 // Flip mask of received word w of one sequence (noise_word's spec) for the wave:
 // thr (< 2^32, > 0) and the key uniform; valid = the word's code bits.
 __device__ __forceinline__ uint32_t noise_word_wave(const GenArgs& a, uint32_t slo, uint32_t nhi, uint32_t w,
@@ -206,8 +238,7 @@ __device__ __forceinline__ uint32_t noise_word_wave(const GenArgs& a, uint32_t s
     philox_blocks<3>(xv, k0, k1);
 #pragma unroll
     for (int gb = 0; gb < 3; ++gb)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) noise_plane_m(xv[gb][e], 0u - ((t >> (31 - 4 * gb - e)) & 1u), U, F);
+      noise_planes4_rt(t >> (28 - 4 * gb), xv[gb][0], xv[gb][1], xv[gb][2], xv[gb][3], U, F);
   }
 #pragma nounroll
   for (int j = 3; j < kNoiseBlocksPerWord; ++j) {
@@ -215,11 +246,7 @@ __device__ __forceinline__ uint32_t noise_word_wave(const GenArgs& a, uint32_t s
     uint32_t k0 = a.k0, k1 = a.k1;
     asm volatile("" : "+s"(k0), "+s"(k1));
     const U4 x = philox(w * kNoiseBlocksPerWord + (uint32_t)j, slo, nhi, a.tag, k0, k1);
-    const uint32_t tj = t << (4 * j);   // thr bits 31 - 4j .. 28 - 4j at the top
-    noise_plane_m(x.x, (uint32_t)((int32_t)tj >> 31), U, F);
-    noise_plane_m(x.y, (uint32_t)((int32_t)(tj << 1) >> 31), U, F);
-    noise_plane_m(x.z, (uint32_t)((int32_t)(tj << 2) >> 31), U, F);
-    noise_plane_m(x.w, (uint32_t)((int32_t)(tj << 3) >> 31), U, F);
+    noise_planes4_rt(t >> (28 - 4 * j), x.x, x.y, x.z, x.w, U, F);   // thr bits 31 - 4j .. 28 - 4j
   }
   return F;
 }
