@@ -327,14 +327,16 @@ struct RowCursor {
   }
   // D_t's key is known: issue the next step's loads
   // kmu8: the key's offset c * 0x11111111, c in {kLo, kLo + 1}
+  // hi: the offset is kLo + 1 (else kLo), as a flag the caller already has
   template <int kLo = 0>
-  __device__ void prefetch(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t rn, uint32_t kmu8 = 0u) {
+  __device__ void prefetch(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t rn, uint32_t kmu8 = 0u,
+                           bool hi = false) {
     if (CVD_ABL & 1) return;
     if (slot >= 0) {
       prefetch_row(a, slot, rn);
     } else if (slot == -2 && !(CVD_ABL & 4)) {
       uint32_t ph, pl;
-      cvd::key_hash_less<kLo>(key_in, NW, kmu8 & 3u, ph, pl);   // = key_hash(key_in - kmu8)
+      cvd::key_hash_less<kLo>(key_in, NW, kLo + (hi ? 1u : 0u), ph, pl);   // = key_hash(key_in - kmu8)
       // byte offsets straight from the hash bits (cvd_keys.h: filter word (pl >> 2) & fmask,
       // pattern (ph >> 2) & (kFilterPatterns - 1)): one AND each
       hs = ph & a.hmask;
@@ -665,7 +667,8 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       }
       // pm: all ones when y has odd parity; the butterflies that decide the
       // pair-swap test are those with out(j, 0) of y's parity
-      const uint32_t pm = 0u - (uint32_t)(__builtin_popcount(rr) & 1u);
+      // (bit rr of 0b0110 is y's parity: one sign-extending bit-field extract)
+      const uint32_t pm = (uint32_t)__builtin_amdgcn_sbfe(6, rr, 1);
       uint32_t hx = 0u, sym = 0u;
       constexpr bool kUniKnown = kSpec, kUni = kSpec && xm_uni<m, XM>();
 #pragma unroll
@@ -689,7 +692,8 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
         for (int v = 0; v < NW; ++v) ck[v] = key[v] - kmu8;
         k1b_trace<m>(a.trace, t, a.nseq, qwave + lane_id(), ck);
       }
-      cur.template prefetch<kSpec && CVD_K1B_LAZYKEY ? 1 : 0>(a, key, rn, kmu8);
+      // the key offset is kLo + mu (lazy) or 0 (eager)
+      cur.template prefetch<kSpec && CVD_K1B_LAZYKEY ? 1 : 0>(a, key, rn, kmu8, CVD_K1B_LAZYKEY && mu != 0u);
     };
 
     // groups of 4 steps (a quarter word): the 10 bits they read (4 words and
