@@ -48,6 +48,7 @@ struct GenArgs {
   uint32_t k0, k1, tag, thr_lo;
   int32_t thr_all, random_input;
   int32_t hs;                     // gen_fast_kernel: history steps ceil(m / k)
+  uint32_t slots;                 // gen_fast_kernel: noise exchange slots per round (64; tests: fewer)
   uint32_t taps[kMaxN][2];        // gen_fast_kernel: shift set of output j on input phase r
   int64_t N, seq_base, seq_stride, pitch, q0, count;
   uint32_t* r;
@@ -147,11 +148,10 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(GenArgs a) {
 //    XOR of W_r >> sh over the host-built tap set taps[j][r] (bit sh), and the
 //    n streams are bit-interleaved into the word (step i in bits n*i .. n*i+n-1).
 //  * Noise: bit-sliced (noise_word, cvd_common.h): the word's bit-planes are
-//    compared with thr for all of its code bits at once, most significant first.
-//    The first three Philox blocks (12 planes) run as one interleaved group; then
-//    one block at a time while any lane of the wave still has an undecided bit
-//    (the wave needs ~3.4 blocks per word on average, against NBITS / 4 = 8 blocks
-//    of one uniform per code bit).
+//    compared with thr for all of its code bits at once, most significant first,
+//    four words at a time with the undecided (lane, word) pairs compacted across
+//    the wave (noise_chunk_wave): ~2.5 Philox blocks per word, against NBITS / 4 =
+//    8 blocks of one uniform per code bit.
 template <int n>
 __device__ __forceinline__ uint32_t spread_n(uint32_t x) {   // bit i -> bit n*i
   if constexpr (n == 1) {
@@ -180,75 +180,113 @@ __device__ __forceinline__ uint32_t even_bits(uint32_t x) {   // bit 2i -> bit i
   return (x | (x >> 8)) & 0x0000FFFFu;
 }
 
-// One bit-plane with thr's bit as a uniform mask pm (0 or ~0): noise_plane
-// without a select, two v_bitop3 (pm in an SGPR) and an or.
-__device__ __forceinline__ void noise_plane_m(uint32_t r, uint32_t pm, uint32_t& U, uint32_t& F) {
-  F |= U & ~r & pm;
-  U &= ~(r ^ pm);
-}
-
-// Four planes against thr's four bits B (most significant first, compile time):
-// the planes' 4-bit value R of each code bit is below B (flip), equal (still
-// undecided) or above (no flip) -- two boolean functions of four inputs that the
-// compiler reduces to a few v_bitop3, instead of three operations per plane.
-template <int B>
-__device__ __forceinline__ void noise_planes4(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& U,
-                                              uint32_t& F) {
+// Four bit-planes r0..r3 (most significant first) against thr's matching 4-bit
+// group `nib` (wave-uniform): the planes' value R of each code bit is below
+// thr's bits (flip), equal (still undecided) or above (no flip).  R < T is a
+// bit-sliced borrow chain over the planes least significant first, borrow' =
+// MAJ(~r, t, borrow): one v_bitop3 per plane with t (0 or ~0) in an SGPR;
+// equality e' = e & ~(r ^ t) is the other.  Two VALU per plane and no branches.
+// (Tried: a 16-way switch over compile-time nibbles needs fewer VALU per case but
+// compiles to a branch tree whose cases copy operands around; per-plane uniform
+// branches were if-converted into selects; the direct MSB-first form with masks
+// costs three VALU per plane.  Measured in profiles/r02z_gen.)
+__device__ __forceinline__ void noise_planes4(uint32_t nib, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
+                                              uint32_t& U, uint32_t& F) {
   const uint32_t r[4] = {r0, r1, r2, r3};
-  uint32_t e = ~0u, l = 0u;   // equal so far / already below
+  const uint32_t b = __builtin_amdgcn_readfirstlane(nib);
+  uint32_t lt = 0u, eq = U;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if ((B >> (3 - i)) & 1) {
-      l |= e & ~r[i];
-      e &= r[i];
-    } else {
-      e &= ~r[i];
-    }
+  for (int i = 3; i >= 0; --i) {
+    const uint32_t ti = 0u - ((b >> (3 - i)) & 1u);
+    // lt = MAJ(~r, t, lt) (truth table 0x8E), eq &= ~(r ^ t) (0x90)
+    asm("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x8e" : "+v"(lt) : "v"(r[i]), "s"(ti));
+    asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x90" : "+v"(eq) : "v"(r[i]), "s"(ti));
   }
-  F |= U & l;
-  U &= e;
-}
-// thr's 4-bit group `nib` (wave-uniform) picks the specialised form
-__device__ __forceinline__ void noise_planes4_rt(uint32_t nib, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
-                                                 uint32_t& U, uint32_t& F) {
-  switch (__builtin_amdgcn_readfirstlane(nib) & 15u) {
-#define CVD_P4(b) case b: noise_planes4<b>(r0, r1, r2, r3, U, F); break;
-    CVD_P4(0) CVD_P4(1) CVD_P4(2) CVD_P4(3) CVD_P4(4) CVD_P4(5) CVD_P4(6) CVD_P4(7)
-    CVD_P4(8) CVD_P4(9) CVD_P4(10) CVD_P4(11) CVD_P4(12) CVD_P4(13) CVD_P4(14) CVD_P4(15)
-#undef CVD_P4
-  }
+  F |= U & lt;
+  U = eq;
 }
 
-// Flip mask of received word w of one sequence (noise_word's spec) for the wave:
-// thr (< 2^32, > 0) and the key uniform; valid = the word's code bits.
-__device__ __forceinline__ uint32_t noise_word_wave(const GenArgs& a, uint32_t slo, uint32_t nhi, uint32_t w,
-                                                    uint32_t valid) {
-  const uint32_t t = a.thr_lo;
-  uint32_t U = valid, F = 0u;
-  {
-    // launder the (uniform) key so its 10-round schedule is recomputed by scalar
-    // adds per group instead of being hoisted into SGPRs
-    uint32_t k0 = a.k0, k1 = a.k1;
-    asm volatile("" : "+s"(k0), "+s"(k1));
-    uint32_t xv[3][4];
+// Per-wave LDS of the straggler exchange: slot records, and every lane's
+// sequence counter words (a slot computes blocks of another lane's sequence)
+struct NoiseLds {
+  uint32_t u[64], m[64], slo[64], nhi[64];
+};
+__device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); __builtin_amdgcn_wave_barrier(); }
+
+// Flip masks F[g] of the words w4 + g (g < 4) of every lane's sequence, noise_word's
+// spec (cvd_common.h) for the wave; live[g] = word exists for this lane.
+//  * Planes 1-8 (Philox blocks 0 and 1) of all four words run unconditionally.  A code
+//    bit is then still undecided with probability 2^-8, so ~12% of the wave's 256
+//    (lane, word) pairs hold one (~30).
+//  * Those pairs are compacted into consecutive lanes through LDS: slot i computes the
+//    next two blocks (8 planes) of the i-th pair and the result goes back to the owner.
+//    After 16 planes ~0.1 undecided bits are left per wave and chunk; a further pass runs
+//    only while the ballot finds one.
+// One word at a time (3 blocks for every lane, then single blocks while any lane is
+// undecided) costs ~3.4 blocks per word; this ~2.5.
+__device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, NoiseLds& sh, uint32_t nhi, uint32_t w4,
+                                                 const bool (&live)[4], uint32_t valid, uint32_t (&F)[4]) {
+  const uint32_t t = a.thr_lo, lane = lane_id();
+  const uint32_t nslots = a.slots - 1u < 64u ? a.slots : 64u;   // 1..64: every round makes progress
+  uint32_t U[4];
 #pragma unroll
-    for (int gb = 0; gb < 3; ++gb) {
-      xv[gb][0] = w * kNoiseBlocksPerWord + (uint32_t)gb; xv[gb][1] = slo; xv[gb][2] = nhi; xv[gb][3] = a.tag;
+  for (int g = 0; g < 4; ++g) { U[g] = live[g] ? valid : 0u; F[g] = 0u; }
+  const uint32_t slo = sh.slo[lane];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {   // blocks 0 and 1 of word g
+    const uint32_t k0 = a.k0, k1 = a.k1;
+    uint32_t xv[2][4];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      xv[b][0] = (w4 + g) * kNoiseBlocksPerWord + (uint32_t)b;
+      xv[b][1] = slo; xv[b][2] = nhi; xv[b][3] = a.tag;
     }
-    philox_blocks<3>(xv, k0, k1);
-#pragma unroll
-    for (int gb = 0; gb < 3; ++gb)
-      noise_planes4_rt(t >> (28 - 4 * gb), xv[gb][0], xv[gb][1], xv[gb][2], xv[gb][3], U, F);
+    philox_blocks<2>(xv, k0, k1);
+    noise_planes4(t >> 28, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U[g], F[g]);
+    noise_planes4(t >> 24, xv[1][0], xv[1][1], xv[1][2], xv[1][3], U[g], F[g]);
   }
 #pragma nounroll
-  for (int j = 3; j < kNoiseBlocksPerWord; ++j) {
-    if (__ballot(U != 0u) == 0ull) break;   // every bit of every lane decided
-    uint32_t k0 = a.k0, k1 = a.k1;
-    asm volatile("" : "+s"(k0), "+s"(k1));
-    const U4 x = philox(w * kNoiseBlocksPerWord + (uint32_t)j, slo, nhi, a.tag, k0, k1);
-    noise_planes4_rt(t >> (28 - 4 * j), x.x, x.y, x.z, x.w, U, F);   // thr bits 31 - 4j .. 28 - 4j
+  for (uint32_t j = 2; j < (uint32_t)kNoiseBlocksPerWord; j += 2) {
+    uint32_t slot[4], tot = 0u;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint64_t b = __ballot(U[g] != 0u);
+      slot[g] = tot + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+      tot += (uint32_t)__builtin_popcountll(b);
+    }
+    if (tot == 0u) break;   // every bit of every pair decided
+#pragma nounroll
+    for (uint32_t s0 = 0; s0 < tot; s0 += nslots) {   // rounds of 64 slots (nearly always one)
+      bool own[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        own[g] = U[g] != 0u && slot[g] - s0 < nslots;
+        if (own[g]) { sh.u[slot[g] - s0] = U[g]; sh.m[slot[g] - s0] = lane | (uint32_t)g << 6; }
+      }
+      wave_lds_sync();
+      const bool busy = lane < nslots && s0 + lane < tot;
+      if (busy) {
+        uint32_t Un = sh.u[lane], Fn = 0u;
+        const uint32_t mm = sh.m[lane], src = mm & 63u, w = w4 + (mm >> 6);
+        const uint32_t k0 = a.k0, k1 = a.k1;
+        uint32_t xv[2][4];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          xv[b][0] = w * kNoiseBlocksPerWord + j + (uint32_t)b;
+          xv[b][1] = sh.slo[src]; xv[b][2] = sh.nhi[src]; xv[b][3] = a.tag;
+        }
+        philox_blocks<2>(xv, k0, k1);
+        noise_planes4(t >> (28u - 4u * j), xv[0][0], xv[0][1], xv[0][2], xv[0][3], Un, Fn);
+        noise_planes4(t >> (24u - 4u * j), xv[1][0], xv[1][1], xv[1][2], xv[1][3], Un, Fn);
+        sh.u[lane] = Un; sh.m[lane] = Fn;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (own[g]) { U[g] = sh.u[slot[g] - s0]; F[g] |= sh.m[slot[g] - s0]; }
+      wave_lds_sync();
+    }
   }
-  return F;
 }
 
 template <int k, int n>
@@ -257,10 +295,17 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   constexpr uint32_t kValid = NBITS == 32 ? ~0u : (1u << (NBITS % 32)) - 1u;
   static_assert(k >= 1 && k <= 2 && SPW * k <= 32, "gen_fast_kernel: shape");
   const int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (li >= a.count) return;
+  // lanes past the end stay in the wave (U = 0, no stores): the noise exchange
+  // uses every lane of the wave as a slot
+  const bool lane_ok = li < a.count;
   const int64_t q = a.q0 + li;
   const uint64_t sid = (uint64_t)(a.seq_base + li * a.seq_stride);
   const uint32_t slo = (uint32_t)sid, nhi = ctr_hi(sid, kKindNoise), ihi = ctr_hi(sid, kKindInput);
+  __shared__ NoiseLds noise_lds[kBlock / 64];
+  NoiseLds& nl = noise_lds[threadIdx.x / 64];
+  nl.slo[lane_id()] = slo;
+  nl.nhi[lane_id()] = nhi;
+  wave_lds_sync();
   const int hs = a.hs;
   const uint32_t hmask = (1u << hs) - 1u;
   const int64_t nwords = (a.N + SPW - 1) / SPW;
@@ -307,13 +352,23 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
     for (int r = 0; r < k; ++r) hist[r] = (Up[r] >> (SPW - hs)) & hmask;
   }
   for (int64_t w4 = 4 * c0; w4 < 4 * c1; w4 += 4) {
+    uint32_t nm4[4] = {0u, 0u, 0u, 0u};
+    bool live[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) live[g] = lane_ok && w4 + g < nwords;
+    if (a.thr_all) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) nm4[g] = kValid;
+    } else if (a.thr_lo) {
+      noise_chunk_wave(a, nl, nhi, (uint32_t)w4, live, kValid, nm4);
+    }
     uint32_t out4[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int64_t w = w4 + g;
       uint32_t word = 0u;
       if (w < nwords) {
-        const uint32_t nm = a.thr_all ? kValid : a.thr_lo ? noise_word_wave(a, slo, nhi, (uint32_t)w, kValid) : 0u;
+        const uint32_t nm = nm4[g];
         uint32_t U[k];
         word_inputs(w, U);
         uint32_t Wr[k];
@@ -349,7 +404,8 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
       }
       out4[g] = word;
     }
-    *reinterpret_cast<uint4*>(a.r + chunk_index(w4 >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
+    if (lane_ok)
+      *reinterpret_cast<uint4*>(a.r + chunk_index(w4 >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
   }
 }
 
@@ -921,6 +977,11 @@ int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t
       for (int b = 0; b < enc.m; ++b)                              // s bit b = u_{b%k}(t - 1 - b/k)
         if ((g >> (1 + b)) & 1u) a.taps[j][b % enc.k] ^= 1u << (a.hs - 1 - b / enc.k);
     }
+  {
+    // test knob: fewer noise exchange slots per round, so the multi-round path runs
+    const char* e = std::getenv("CVD_GEN_SLOTS");
+    a.slots = e ? (uint32_t)std::min(64, std::max(1, std::atoi(e))) : 64u;
+  }
   const bool fast = !std::getenv("CVD_GEN_GENERIC") && enc.m <= kMaxM && a.hs + 32 / std::max(enc.n, 1) <= 32;
   auto kern = gen_kernel<0, 0>;
   dim3 gdim(grid);

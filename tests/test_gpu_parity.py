@@ -84,6 +84,27 @@ def test_fast_generator_equals_generic_long(pkg, golden, dev, name, monkeypatch)
         np.testing.assert_array_equal(got[:, q], want)
 
 
+@pytest.mark.parametrize("slots", [1, 5, 17])
+def test_fast_generator_noise_exchange_rounds(pkg, golden, dev, slots, monkeypatch):
+    """The wave's undecided (sequence, word) pairs are finished by slot lanes in
+    rounds of 64 (noise_chunk_wave); with ~30 pairs per chunk a second round almost
+    never runs.  CVD_GEN_SLOTS shrinks the round so that the multi-round path runs,
+    on a ragged wave count, and must give the same stream."""
+    z, meta = golden
+    k, n, m, taps = code_of(meta, "m2_75")
+    det = pkg.Detector(k, n, m, taps, device=0)
+    N, p, seed, count = 20_011, 0.2, 7, 200
+    tag = philox.grid_tag(N, p)
+    ref = det.generate(taps, N, p, seed, tag, 3, 1, count)
+    monkeypatch.setenv("CVD_GEN_SLOTS", str(slots))
+    got = det.generate(taps, N, p, seed, tag, 3, 1, count)
+    monkeypatch.delenv("CVD_GEN_SLOTS")
+    assert torch.equal(got, ref)
+    words = unpack_words(got, n, N)
+    for q in (0, 77, count - 1):
+        np.testing.assert_array_equal(words[:, q], R.received_stream(taps, m, k, n, N, p, seed, tag, 3 + q))
+
+
 # ───────────────────────────── metric trace ─────────────────────────────────
 
 @pytest.mark.parametrize("name", ["m2_75", "m3_demo", "r23_m4", "m6_133_171"])
