@@ -257,12 +257,9 @@ __device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, NoiseLds& sh,
     if (tot == 0u) break;   // every bit of every pair decided
 #pragma nounroll
     for (uint32_t s0 = 0; s0 < tot; s0 += nslots) {   // rounds of 64 slots (nearly always one)
-      bool own[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        own[g] = U[g] != 0u && slot[g] - s0 < nslots;
-        if (own[g]) { sh.u[slot[g] - s0] = U[g]; sh.m[slot[g] - s0] = lane | (uint32_t)g << 6; }
-      }
+      for (int g = 0; g < 4; ++g)
+        if (U[g] != 0u && slot[g] - s0 < nslots) { sh.u[slot[g] - s0] = U[g]; sh.m[slot[g] - s0] = lane | (uint32_t)g << 6; }
       wave_lds_sync();
       const bool busy = lane < nslots && s0 + lane < tot;
       if (busy) {
@@ -282,8 +279,8 @@ __device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, NoiseLds& sh,
       }
       wave_lds_sync();
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        if (own[g]) { U[g] = sh.u[slot[g] - s0]; F[g] |= sh.m[slot[g] - s0]; }
+      for (int g = 0; g < 4; ++g)   // owners (U still holds the value they sent)
+        if (U[g] != 0u && slot[g] - s0 < nslots) { U[g] = sh.u[slot[g] - s0]; F[g] |= sh.m[slot[g] - s0]; }
       wave_lds_sync();
     }
   }
