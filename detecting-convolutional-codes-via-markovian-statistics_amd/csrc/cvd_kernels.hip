@@ -304,7 +304,6 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   nl.nhi[lane_id()] = nhi;
   wave_lds_sync();
   const int hs = a.hs;
-  const uint32_t hmask = (1u << hs) - 1u;
   const int64_t nwords = (a.N + SPW - 1) / SPW;
   const int64_t nw4 = (nwords + 3) & ~(int64_t)3;
   int64_t iblk = -1;
@@ -339,15 +338,29 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   // independent (more waves in flight than one lane per sequence gives)
   const int64_t nchunks = nw4 >> 2, seg = gridDim.y;
   const int64_t c0 = nchunks * blockIdx.y / seg, c1 = nchunks * (blockIdx.y + 1) / seg;
-  uint32_t hist[k];
+  // k = 1 (spread-first): the input bits are Morton-spread once per word (bit i ->
+  // bit n*i), and the window W = U << hs | (history) is kept in that spread form as
+  // 64 bits (lo, hi): every tap W >> sh is then one v_alignbit by n*sh of (hi, lo),
+  // already at the output's bit positions, so the n outputs need no spread of their
+  // own (m2 generator 12.1 -> 11.6 ms, m = 6 8.6 -> 8.3 ms alone).  sprev: the
+  // previous word's spread inputs (the history is its top hs steps).
+  // k = 2 keeps plain windows and one spread per output: spread-first made the
+  // rate-2/3 generator faster alone (16.1 -> 15.8 ms) but the overlapped C3 step
+  // 1.7% slower (profiles/r02z_gen/ab_enc_*.json).
+  constexpr bool kSpreadFirst = k == 1;
+  uint32_t sprev[k], hist[k];
 #pragma unroll
-  for (int r = 0; r < k; ++r) hist[r] = 0u;   // encoder starts in state 0
+  for (int r = 0; r < k; ++r) sprev[r] = hist[r] = 0u;   // encoder starts in state 0
   if (c0 > 0 && 4 * c0 <= nwords) {
     uint32_t Up[k];
     word_inputs(4 * c0 - 1, Up);
 #pragma unroll
-    for (int r = 0; r < k; ++r) hist[r] = (Up[r] >> (SPW - hs)) & hmask;
+    for (int r = 0; r < k; ++r) {
+      if constexpr (kSpreadFirst) sprev[r] = spread_n<n>(Up[r]);
+      else hist[r] = (Up[r] >> (SPW - hs)) & ((1u << hs) - 1u);
+    }
   }
+  const uint32_t nhs = (uint32_t)(n * hs), nrest = (uint32_t)(n * (SPW - hs));   // 0 < nhs < 32, nrest < 32
   for (int64_t w4 = 4 * c0; w4 < 4 * c1; w4 += 4) {
     uint32_t nm4[4] = {0u, 0u, 0u, 0u};
     bool live[4];
@@ -368,11 +381,19 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
         const uint32_t nm = nm4[g];
         uint32_t U[k];
         word_inputs(w, U);
-        uint32_t Wr[k];
+        uint32_t lo[k], hi[k];   // spread-first windows, or the plain windows in lo
 #pragma unroll
         for (int r = 0; r < k; ++r) {
-          Wr[r] = (U[r] << hs) | hist[r];
-          hist[r] = (Wr[r] >> SPW) & hmask;
+          if constexpr (kSpreadFirst) {
+            const uint32_t su = spread_n<n>(U[r]);
+            lo[r] = (su << nhs) | (sprev[r] >> nrest);
+            hi[r] = su >> (32u - nhs);
+            sprev[r] = su;
+          } else {
+            lo[r] = (U[r] << hs) | hist[r];
+            hi[r] = 0u;
+            hist[r] = (lo[r] >> SPW) & ((1u << hs) - 1u);
+          }
         }
 #pragma unroll
         for (int j = 0; j < n; ++j) {
@@ -389,12 +410,18 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
             while (tm) {
               const uint32_t sh = (uint32_t)__builtin_ctz(tm);
               tm &= tm - 1u;
-              o ^= Wr[r] >> sh;
+              if constexpr (kSpreadFirst) o ^= __builtin_amdgcn_alignbit(hi[r], lo[r], (uint32_t)n * sh);
+              else o ^= lo[r] >> sh;
             }
           }
-          if constexpr (SPW < 32) o &= (1u << SPW) - 1u;
-          word |= spread_n<n>(o) << j;
+          if constexpr (kSpreadFirst) {
+            word |= o << j;
+          } else {
+            if constexpr (SPW < 32) o &= (1u << SPW) - 1u;
+            word |= spread_n<n>(o) << j;
+          }
         }
+        if constexpr (kSpreadFirst && NBITS < 32) word &= kValid;   // n = 3: step SPW's bits at 30, 31
         word ^= nm;
         const int64_t ns = a.N - w * SPW;           // steps in this word (last word: < SPW)
         if (ns < SPW) word &= (1u << (n * ns)) - 1u;
