@@ -252,7 +252,8 @@ struct RowCursor {
     pnx = ld_off<int32_t>(reinterpret_cast<const char*>(a.hrow) + 8u * R, o_nx);
   }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
-    slot = a.slot0; hs = 0u; fb = 0u; fw = 0u; cand = false;
+    // (CVD_ABL & 4: a pattern no filter word passes, so no lane ever becomes a candidate)
+    slot = a.slot0; hs = 0u; fb = (CVD_ABL & 4) ? 1u : 0u; fw = 0u; cand = false;
     if (CVD_ABL & 1) return;
     prefetch_row(a, slot, r0);
   }
