@@ -616,17 +616,28 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     uint32_t kmu8 = kSpec && CVD_K1B_LAZYKEY ? 0x11111111u : 0u;   // nibble offset of the stored key
     if constexpr (kTrace) k1b_trace<m>(a.trace, 0, a.nseq, qwave + lane_id(), key);
     // Received words: word w of this sequence at rbase + (w/4)*cstride + w%4
-    // (16-byte chunks, include/cvd.h).  Only the current word and the next are
-    // held; the next is loaded when the current one starts, 12 steps before its
-    // first use (the last group of the current word reads its first step).
+    // (16-byte chunks, include/cvd.h).  A lane reads its whole chunk at once
+    // (one 16-byte load per 64 steps): read a word at a time, the wave's 1 KiB of
+    // chunk lines was fetched from HBM up to four times, once per word.  c4 holds
+    // the chunk of the next word; it is loaded when the last word of the current
+    // chunk starts, 12 steps before its first use (the last group of a word reads
+    // the next word's first step).  cw is the current word.
     const int64_t N = a.N, nwords = (N + 15) / 16;
     const size_t cstride = (size_t)a.nseq * 4;   // dwords between chunks of one sequence
-    auto load_word = [&](int64_t wi) -> uint32_t {   // lane address recomputed: no live VGPR pair
-      const uint32_t* rb = a.r + (size_t)(wi >> 2) * cstride + (size_t)(wi & 3) + (size_t)qwave * 4;
-      return wi < nwords ? rb[lane_id() * 4u] : 0u;
+    uint32_t c4[4];
+    auto load_chunk = [&](int64_t ci) {   // lane address recomputed: no live VGPR pair
+      const uint32_t* rb = a.r + (size_t)ci * cstride + (size_t)qwave * 4;
+      const uint4 v = 4 * ci < nwords ? *reinterpret_cast<const uint4*>(rb + lane_id() * 4u) : make_uint4(0u, 0u, 0u, 0u);
+      c4[0] = v.x; c4[1] = v.y; c4[2] = v.z; c4[3] = v.w;
     };
-    uint32_t cw = load_word(0);     // current word
-    uint32_t nw = load_word(1);     // next word
+    // word wi of c4 (wi wave-uniform: three selects on an SGPR index), 0 past the stream
+    auto pick = [&](int64_t wi) -> uint32_t {
+      const uint32_t e = (uint32_t)wi & 3u;
+      const uint32_t v = e == 0u ? c4[0] : e == 1u ? c4[1] : e == 2u ? c4[2] : c4[3];
+      return wi < nwords ? v : 0u;
+    };
+    load_chunk(0);
+    uint32_t cw = pick(0);          // current word
     int64_t w = 0;                  // index of the current word
     RowCursor<NW, R> cur;
     cur.start(a, cw & 3u);
@@ -704,16 +715,16 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     int g = 0;
     int dec = 0;   // early decision of this lane (0 = open)
     for (; t + 4 <= N; t += 4) {
-      const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(nw, cw, 24);
+      const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(pick(w + 1), cw, 24);
       step(bits2(win, 0), bits2(win, 2), t + 1, IntC<1>{});
       step(bits2(win, 2), bits2(win, 4), t + 2, IntC<2>{});
       step(bits2(win, 4), bits2(win, 6), t + 3, IntC<1>{});
       step(bits2(win, 6), bits2(win, 8), t + 4, IntC<2>{});
       if (++g == 4) {
         g = 0;
-        cw = nw;
         ++w;
-        nw = load_word(w + 1);
+        cw = pick(w);
+        if (((w + 1) & 3) == 0) load_chunk((w + 1) >> 2);   // the next word opens a chunk
       }
       if (((t + 4) & (kRenorm - 1)) == 0) {
         if constexpr (!kSpec) {
@@ -735,7 +746,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     }
     // last 1-3 steps (inside the current group, so no renormalisation is due)
     if (t < N) {
-      const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(nw, cw, 24);
+      const uint32_t win = g < 3 ? cw >> (8 * g) : __builtin_amdgcn_alignbit(pick(w + 1), cw, 24);
       step(bits2(win, 0), bits2(win, 2), t + 1, IntC<1>{});
       if (t + 1 < N) step(bits2(win, 2), bits2(win, 4), t + 2, IntC<2>{});
       if (t + 2 < N) step(bits2(win, 4), bits2(win, 6), t + 3, IntC<1>{});
