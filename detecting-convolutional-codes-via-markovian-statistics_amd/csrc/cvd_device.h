@@ -206,7 +206,9 @@ __device__ __forceinline__ void fill_filter_patterns() {
 
 // Ablation knobs for timing studies only (profiles/ab_k1b.py --no-check; results
 // differ): bit 0 drops the P̂1 row lookup, bit 1 the T_ref count, bit 2 the
-// hashed lookup of states outside the learned rows (table mode only).
+// hashed lookup of states outside the learned rows (table mode only), bit 4 the
+// table walk after a hashed hit (the lane hashes again), bit 5 the key and record
+// reads of filter-positive lanes (hash and filter test only).
 #ifndef CVD_ABL
 #define CVD_ABL 0
 #endif
@@ -273,7 +275,7 @@ struct RowCursor {
   }
   __device__ void mid(const ExpArgs& a, uint32_t r) {
     if (CVD_ABL & 1) return;
-    cand = slot == -2 && (fw & fb) == fb;
+    cand = slot == -2 && (fw & fb) == fb && !(CVD_ABL & 32);
     if (cand) {
 #pragma unroll
       for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs * NW + w) * 4u);
@@ -304,7 +306,7 @@ struct RowCursor {
 #pragma unroll
       for (int w = 0; w < NW; ++w) key[w] = key_in[w] - kmu8;
       if (same_key(pkey, key)) {
-        lpv = plp; ns = pnx;
+        lpv = plp; ns = (CVD_ABL & 16) ? -2 : pnx;
       } else if (pkey[0] != kEmptyKey) {
         // home slot holds another row: linear probing up to an empty slot
         uint32_t sl = hs;
