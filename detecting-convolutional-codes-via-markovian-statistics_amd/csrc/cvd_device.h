@@ -143,6 +143,7 @@ struct ExpArgs {
   uint32_t bfly_uni;        // k = 1 butterfly kernel: every out(j, 0), j < 2^(m-1), in one class
   uint32_t bfly_even[4];    // k = 1 butterfly kernel: nibble masks of the butterflies with out(j, 0) in {00, 11}
   uint32_t hmask, fmask, fmask4;   // fmask4 = fmask << 2 (filter byte offsets)
+  uint32_t ksh, rsh;        // directory slot strides as byte shifts: key (hkey), record (hrow)
   int32_t max_probe;
   int32_t slot0;            // row of D_0 = 0
   double lp_unseen;
@@ -249,7 +250,7 @@ struct RowCursor {
   }
   __device__ void prefetch_dir(const ExpArgs& a, int32_t s, uint32_t rn) {
     uint32_t o_lp, o_nx;
-    rec_offsets((uint32_t)s * RSB, rn, o_lp, o_nx);
+    rec_offsets((uint32_t)s << a.rsh, rn, o_lp, o_nx);
     plp = ld_off<double>(a.hrow, o_lp);
     pnx = ld_off<int32_t>(reinterpret_cast<const char*>(a.hrow) + 8u * R, o_nx);
   }
@@ -278,7 +279,7 @@ struct RowCursor {
     cand = slot == -2 && (fw & fb) == fb && !(CVD_ABL & 32);
     if (cand) {
 #pragma unroll
-      for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs * NW + w) * 4u);
+      for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs << a.ksh) + 4u * w);
       prefetch_dir(a, (int32_t)hs, r);
     }
   }
@@ -315,13 +316,13 @@ struct RowCursor {
           sl = (sl + 1u) & a.hmask;
           uint32_t k[NW];
 #pragma unroll
-          for (int w = 0; w < NW; ++w) k[w] = ld_off<uint32_t>(a.hkey, (sl * NW + w) * 4u);
+          for (int w = 0; w < NW; ++w) k[w] = ld_off<uint32_t>(a.hkey, (sl << a.ksh) + 4u * w);
           if (k[0] == kEmptyKey) break;
           if (same_key(k, key)) { found = true; break; }
         }
         if (found) {
-          lpv = ld_off<double>(a.hrow, sl * RSB + 8u * r);
-          ns = ld_off<int32_t>(a.hrow, sl * RSB + 4u * (2u * R + r));
+          lpv = ld_off<double>(a.hrow, (sl << a.rsh) + 8u * r);
+          ns = ld_off<int32_t>(a.hrow, (sl << a.rsh) + 4u * (2u * R + r));
         }
       }
     }

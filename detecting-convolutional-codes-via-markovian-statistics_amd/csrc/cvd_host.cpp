@@ -490,9 +490,22 @@ void build_hash(cvd_model& Mo) {
   while ((fscale >= 0 ? fcap >> fscale : fcap << -fscale) < Mo.n_rows && fcap < ((int64_t)1 << fmax_log2)) fcap <<= 1;
   Mo.fcap = fcap;
   Mo.h_filt.assign((size_t)fcap, 0u);
-  Mo.h_key.assign((size_t)cap * nw, kEmptyKey);
   Mo.h_rsw = row_words(Mo.dec.n);
-  Mo.h_row.assign((size_t)cap * Mo.h_rsw, 0u);
+  // Key and record of a slot in one power-of-two slot (128 B at m = 6, n = 2): a
+  // hit reads one line instead of a key line and a record line (p = 0.1 launch
+  // 3,122 -> 2,969 ms, profiles/r02z5_il/).  h_row stays empty and the device
+  // record base is the key base + nw dwords.  CVD_SLOT_IL=0: separate key and
+  // record arrays (timing studies).
+  const char* il = std::getenv("CVD_SLOT_IL");
+  const bool interleave = !(il && std::atoi(il) == 0);
+  int ssw = nw;
+  if (interleave)
+    for (ssw = 1; ssw < nw + Mo.h_rsw;) ssw <<= 1;
+  Mo.h_ssw = ssw;
+  if (cap * (int64_t)ssw * 4 > ((int64_t)1 << 32))
+    throw std::length_error("explicit-path row table over 4 GiB (too many learned rows)");
+  Mo.h_key.assign((size_t)cap * ssw, kEmptyKey);
+  Mo.h_row.assign(interleave ? 0 : (size_t)cap * Mo.h_rsw, 0u);
   Mo.h_drow.assign((size_t)Mo.n_rows * Mo.h_rsw, 0u);
   Mo.max_probe = 0;
   std::vector<int64_t> slot_of((size_t)Mo.n_rows);
@@ -510,9 +523,9 @@ void build_hash(cvd_model& Mo) {
     Mo.h_filt[(size_t)filter_word_index(pl, (uint32_t)(fcap - 1))] |= filter_pattern(filter_pattern_index(ph));
     uint64_t slot = ph & (uint64_t)(cap - 1);
     int probe = 0;
-    while (Mo.h_key[slot * nw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
+    while (Mo.h_key[slot * ssw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
     Mo.max_probe = std::max(Mo.max_probe, probe);
-    for (int w = 0; w < nw; ++w) Mo.h_key[slot * nw + w] = kw[w];
+    for (int w = 0; w < nw; ++w) Mo.h_key[slot * ssw + w] = kw[w];
     slot_of[(size_t)i] = (int64_t)slot;
   }
   parallel_for(Mo.n_rows, [&](int64_t i, int) {
@@ -522,7 +535,9 @@ void build_hash(cvd_model& Mo) {
       const int64_t j = Mo.row_next[(size_t)i * R + r];
       dw[2 * R + r] = (uint32_t)(j >= 0 ? (int32_t)j : -1);
     }
-    std::memcpy(Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw, dw, sizeof(uint32_t) * Mo.h_rsw);
+    uint32_t* hw = interleave ? Mo.h_key.data() + (size_t)slot_of[(size_t)i] * ssw + nw
+                              : Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw;
+    std::memcpy(hw, dw, sizeof(uint32_t) * Mo.h_rsw);
   });
   Mo.slot0 = 0;   // D_0 = 0 is row 0 in both model kinds
 }

@@ -36,6 +36,7 @@ struct cvd_model {
   int64_t fcap = 0;               // filter words, power of two
   std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector, word 0 = kEmptyKey if empty
   int32_t h_rsw = 0;              // row record stride in dwords (row_words)
+  int32_t h_ssw = 0;              // directory slot stride in dwords: nw, or (CVD_SLOT_IL) key + record in one slot
   std::vector<uint32_t> h_row;    // [hcap][h_rsw]: log P̂1[r] (2^n f64), successor row[r] (2^n i32, -1: none)
   std::vector<uint32_t> h_drow;   // [n_rows][h_rsw]: the same records dense by row id (table mode)
   int32_t slot0 = 0;              // row of D_0 = 0 (always 0)

@@ -1097,7 +1097,12 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   }
   if (nseq <= 0) return CVD_OK;
   ExpArgs a;
-  a.filt = M.d_filt; a.hkey = M.d_hkey; a.hrow = M.d_hrow; a.drow = M.d_drow; a.ltref = M.d_ltref;
+  a.filt = M.d_filt; a.hkey = M.d_hkey; a.drow = M.d_drow; a.ltref = M.d_ltref;
+  // directory slots: keys [hcap][h_ssw dwords], records [hcap][h_rsw] or, interleaved
+  // (no separate record array), at dword nw of each key slot
+  a.hrow = M.d_hrow ? M.d_hrow : M.d_hkey + nib_words(M.dec.m);
+  a.ksh = (uint32_t)__builtin_ctz((unsigned)(4 * M.h_ssw));
+  a.rsh = M.d_hrow ? (uint32_t)__builtin_ctz((unsigned)(4 * M.h_rsw)) : a.ksh;
   a.bmp = bmp; a.slot0 = M.slot0;
   a.repmap = M.repmap; a.swmap = M.swmap; a.bfly_uni = M.bfly_uni;
   for (int w = 0; w < 4; ++w) a.bfly_even[w] = M.bfly_even[w];
