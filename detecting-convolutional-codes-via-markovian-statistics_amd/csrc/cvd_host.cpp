@@ -468,12 +468,32 @@ void build_hash(cvd_model& Mo) {
   //  * the same records dense by row id (h_drow), which a sequence walking
   //    learned rows reads without hashing (table mode): the rows a walk visits
   //    sit together in first-visit order instead of scattered over the
-  //    directory (load <= 1/8).
+  //    directory (load <= 1/16).
   const int m = Mo.dec.m, M = 1 << m, R = 1 << Mo.dec.n, nw = nib_words(m);
+  Mo.h_rsw = row_words(Mo.dec.n);
+  // Key and record of a slot in one power-of-two slot (128 B at m = 6, n = 2): a
+  // hit reads one line instead of a key line and a record line (p = 0.1 launch
+  // 3,122 -> 2,969 ms, profiles/r02z5_il/).  h_row stays empty and the device
+  // record base is the key base + nw dwords.  CVD_SLOT_IL=0: separate key and
+  // record arrays (timing studies).
+  const char* il = std::getenv("CVD_SLOT_IL");
+  const bool interleave = !(il && std::atoi(il) == 0);
+  int ssw = nw;
+  if (interleave)
+    for (ssw = 1; ssw < nw + Mo.h_rsw;) ssw <<= 1;
+  Mo.h_ssw = ssw;
+  // Load factor <= 1/16: a hit is at its home slot ~97% of the time, and every
+  // probe past it is a dependent line read (p = 0.1: 2,972 ms at 1/8, 2,925 at
+  // 1/16, 3,095 at 1/4, profiles/r02z6_dir/).  Device offsets are 32-bit byte
+  // offsets, so a table past 4 GiB runs at a higher load (down to 1/2).
+  // (CVD_DIR_LOAD_LOG2=s: load <= 2^-s, for timing studies)
+  int load_log2 = 4;
+  if (const char* e = std::getenv("CVD_DIR_LOAD_LOG2")) load_log2 = std::max(1, std::min(5, std::atoi(e)));
   int64_t cap = 64;
-  while (cap < 8 * Mo.n_rows) cap <<= 1;   // load factor <= 1/8: a hit is at its home slot ~94% of the time
-  // device offsets are 32-bit byte offsets into the row records
-  if (cap * (int64_t)row_words(Mo.dec.n) * 4 > ((int64_t)1 << 32))
+  while (cap < ((int64_t)1 << load_log2) * Mo.n_rows) cap <<= 1;
+  const int64_t slot_bytes = 4 * (int64_t)std::max(ssw, interleave ? 0 : Mo.h_rsw);
+  while (cap * slot_bytes > ((int64_t)1 << 32) && cap / 2 >= 2 * Mo.n_rows && cap > 64) cap >>= 1;
+  if (cap * slot_bytes > ((int64_t)1 << 32) || cap < 2 * Mo.n_rows)
     throw std::length_error("explicit-path row table over 4 GiB (too many learned rows)");
   Mo.hcap = cap;
   int64_t fcap = 64;
@@ -490,20 +510,6 @@ void build_hash(cvd_model& Mo) {
   while ((fscale >= 0 ? fcap >> fscale : fcap << -fscale) < Mo.n_rows && fcap < ((int64_t)1 << fmax_log2)) fcap <<= 1;
   Mo.fcap = fcap;
   Mo.h_filt.assign((size_t)fcap, 0u);
-  Mo.h_rsw = row_words(Mo.dec.n);
-  // Key and record of a slot in one power-of-two slot (128 B at m = 6, n = 2): a
-  // hit reads one line instead of a key line and a record line (p = 0.1 launch
-  // 3,122 -> 2,969 ms, profiles/r02z5_il/).  h_row stays empty and the device
-  // record base is the key base + nw dwords.  CVD_SLOT_IL=0: separate key and
-  // record arrays (timing studies).
-  const char* il = std::getenv("CVD_SLOT_IL");
-  const bool interleave = !(il && std::atoi(il) == 0);
-  int ssw = nw;
-  if (interleave)
-    for (ssw = 1; ssw < nw + Mo.h_rsw;) ssw <<= 1;
-  Mo.h_ssw = ssw;
-  if (cap * (int64_t)ssw * 4 > ((int64_t)1 << 32))
-    throw std::length_error("explicit-path row table over 4 GiB (too many learned rows)");
   Mo.h_key.assign((size_t)cap * ssw, kEmptyKey);
   Mo.h_row.assign(interleave ? 0 : (size_t)cap * Mo.h_rsw, 0u);
   Mo.h_drow.assign((size_t)Mo.n_rows * Mo.h_rsw, 0u);

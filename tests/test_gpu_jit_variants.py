@@ -41,3 +41,33 @@ def test_lazy_key_variants_bit_identical(pkg, dev, p, monkeypatch):
     cm = C.Model(c1, p, None, 200, 1.0, SEED)
     _, s_cpu = cm.run_trials(c1, c2, N, p, SEED, t0, t0 + 16, sums=True)
     assert np.array_equal(ref[:16], s_cpu)
+
+
+def _dir_sums(pkg, det, cc, p, N, T, t0, env, monkeypatch):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    model = pkg.Model(det.dec, p, None, 200, 1.0, SEED).upload(0)
+    for k in env:
+        monkeypatch.delenv(k)
+    return model, det.run_trials(model, cc["gen1"], cc["gen2"], N, p, SEED, t0, t0 + T, return_sums=True)["sums"]
+
+
+@pytest.mark.parametrize("p", [0.02, 0.1])
+def test_directory_layouts_bit_identical(pkg, dev, p, monkeypatch):
+    """Directory layouts (csrc/cvd_host.cpp build_hash): key and record in one slot
+    (default) or in two arrays (CVD_SLOT_IL=0), at load 1/16 (default) and 1/2
+    (CVD_DIR_LOAD_LOG2=1: most hits probe past the home slot)."""
+    cc = pkg.CONFIG_CODES["m6"]
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    N, T, t0 = 20_000, 2048, 4242
+    m0, ref = _dir_sums(pkg, det, cc, p, N, T, t0, {}, monkeypatch)
+    assert m0.info()["hash_capacity"] >= 16 * m0.info()["n_rows"]
+    for env in ({"CVD_SLOT_IL": "0"}, {"CVD_DIR_LOAD_LOG2": "1"}, {"CVD_SLOT_IL": "0", "CVD_DIR_LOAD_LOG2": "1"}):
+        mv, got = _dir_sums(pkg, det, cc, p, N, T, t0, env, monkeypatch)
+        if "CVD_DIR_LOAD_LOG2" in env:
+            assert mv.info()["hash_capacity"] < 4 * mv.info()["n_rows"] and mv.info()["max_probe"] > 1
+        assert np.array_equal(got, ref), env
+    c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
+    cm = C.Model(c1, p, None, 200, 1.0, SEED)
+    _, s_cpu = cm.run_trials(c1, c2, N, p, SEED, t0, t0 + 16, sums=True)
+    assert np.array_equal(ref[:16], s_cpu)
