@@ -133,7 +133,7 @@ constexpr int kEarlyEvery = 128;   // steps between checks (the k = 1 butterfly 
 // ────────────────────────── explicit metric path ────────────────────────────
 
 struct ExpArgs {
-  const uint32_t* filt;     // [fmask + 1] Bloom filter words over the row keys (filter_pattern)
+  const uint32_t* filt;     // [fmask + 1][2] Bloom filter blocks over the row keys (filter_pattern)
   const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors, word 0 = kEmptyKey if empty
   const uint32_t* hrow;     // [hcap][row_words(n)]: log P̂1[r] (f64), successor row[r] (i32, -1 = not a row)
   const uint32_t* drow;     // [rows][row_words(n)]: the same records dense by row id (table mode)
@@ -142,7 +142,7 @@ struct ExpArgs {
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
   uint32_t bfly_uni;        // k = 1 butterfly kernel: every out(j, 0), j < 2^(m-1), in one class
   uint32_t bfly_even[4];    // k = 1 butterfly kernel: nibble masks of the butterflies with out(j, 0) in {00, 11}
-  uint32_t hmask, fmask, fmask4;   // fmask4 = fmask << 2 (filter byte offsets)
+  uint32_t hmask, fmask, fmask4;   // fmask: filter blocks - 1, fmask4 = fmask << 3 (block byte offsets)
   uint32_t ksh, rsh;        // directory slot strides as byte shifts: key (hkey), record (hrow)
   int32_t max_probe;
   int32_t slot0;            // row of D_0 = 0
@@ -229,7 +229,7 @@ template <int NW, int R>
 struct RowCursor {
   static constexpr uint32_t RSB = 4u * row_words_c(R);   // record bytes
   int32_t slot, pnx;
-  uint32_t hs, fb, fw;
+  uint32_t hs, fb, fw, fb1, fw1;   // filter block words and their patterns
   bool cand;
   double plp;
   uint32_t pkey[NW];
@@ -256,7 +256,7 @@ struct RowCursor {
   }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
     // (CVD_ABL & 4: a pattern no filter word passes, so no lane ever becomes a candidate)
-    slot = a.slot0; hs = 0u; fb = (CVD_ABL & 4) ? 1u : 0u; fw = 0u; cand = false;
+    slot = a.slot0; hs = 0u; fb = (CVD_ABL & 4) ? 1u : 0u; fw = 0u; fb1 = 0u; fw1 = 0u; cand = false;
     if (CVD_ABL & 1) return;
     prefetch_row(a, slot, r0);
   }
@@ -267,7 +267,7 @@ struct RowCursor {
   // that consumes an ACS result (the running zero-nibble test, which depends on
   // every butterfly computed so far), so the waits land after that much work.
   __device__ void fence(uint32_t dep) {
-    asm volatile("" : "+v"(fw), "+v"(slot), "+v"(pnx), "+v"(plp) : "v"(dep));
+    asm volatile("" : "+v"(fw), "+v"(fw1), "+v"(slot), "+v"(pnx), "+v"(plp) : "v"(dep));
   }
   template <int N_>
   __device__ void fence_keys(uint32_t dep) {
@@ -276,7 +276,7 @@ struct RowCursor {
   }
   __device__ void mid(const ExpArgs& a, uint32_t r) {
     if (CVD_ABL & 1) return;
-    cand = slot == -2 && (fw & fb) == fb && !(CVD_ABL & 32);
+    cand = slot == -2 && ((fb & ~fw) | (fb1 & ~fw1)) == 0u && !(CVD_ABL & 32);
     if (cand) {
 #pragma unroll
       for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs << a.ksh) + 4u * w);
@@ -341,12 +341,15 @@ struct RowCursor {
     } else if (slot == -2 && !(CVD_ABL & 4)) {
       uint32_t ph, pl;
       cvd::key_hash_less<kLo>(key_in, NW, kLo + (hi ? 1u : 0u), ph, pl);   // = key_hash(key_in - kmu8)
-      // byte offsets straight from the hash bits (cvd_keys.h: filter word (pl >> 2) & fmask,
-      // pattern (ph >> 2) & (kFilterPatterns - 1)): one AND each
+      // byte offsets straight from the hash bits (cvd_keys.h: filter block (pl >> 3) & fmask,
+      // patterns (ph >> 2) and (ph >> 14) & (kFilterPatterns - 1))
       hs = ph & a.hmask;
-      fb = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(filter_patterns_lds()) +
-                                              (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 2)));
-      fw = ld_off<uint32_t>(a.filt, pl & a.fmask4);
+      const char* pt = reinterpret_cast<const char*>(filter_patterns_lds());
+      fb = *reinterpret_cast<const uint32_t*>(pt + (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 2)));
+      fb1 = *reinterpret_cast<const uint32_t*>(pt + ((ph >> 12) & (uint32_t)((cvd::kFilterPatterns - 1) << 2)));
+      const uint2 f = ld_off<uint2>(a.filt, pl & a.fmask4);
+      fw = f.x;
+      fw1 = f.y;
     }
   }
 };

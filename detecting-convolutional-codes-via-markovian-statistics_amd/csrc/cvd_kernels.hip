@@ -1106,7 +1106,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   a.bmp = bmp; a.slot0 = M.slot0;
   a.repmap = M.repmap; a.swmap = M.swmap; a.bfly_uni = M.bfly_uni;
   for (int w = 0; w < 4; ++w) a.bfly_even[w] = M.bfly_even[w];
-  a.hmask = (uint32_t)(M.hcap - 1); a.fmask = (uint32_t)(M.fcap - 1); a.fmask4 = a.fmask << 2; a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
+  a.hmask = (uint32_t)(M.hcap - 1); a.fmask = (uint32_t)(M.fcap / 2 - 1); a.fmask4 = a.fmask << 3; a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   a.trace = d_trace;
   a.early = early && !d_sums && !d_trace; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
