@@ -274,12 +274,25 @@ struct RowCursor {
 #pragma unroll
     for (int w = 0; w < N_; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
   }
+  // key of directory slot s: 16-byte loads when the key is whole 16-byte pieces (a
+  // slot's key is aligned to its power-of-two stride), else dword loads
+  __device__ static void load_key(const ExpArgs& a, uint32_t s, uint32_t (&k)[NW]) {
+    if constexpr (NW % 4 == 0) {
+#pragma unroll
+      for (int i = 0; i < NW / 4; ++i) {
+        const uint4 v = ld_off<uint4>(a.hkey, (s << a.ksh) + 16u * i);
+        k[4 * i] = v.x; k[4 * i + 1] = v.y; k[4 * i + 2] = v.z; k[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) k[w] = ld_off<uint32_t>(a.hkey, (s << a.ksh) + 4u * w);
+    }
+  }
   __device__ void mid(const ExpArgs& a, uint32_t r) {
     if (CVD_ABL & 1) return;
     cand = slot == -2 && ((fb & ~fw) | (fb1 & ~fw1)) == 0u && !(CVD_ABL & 32);
     if (cand) {
-#pragma unroll
-      for (int w = 0; w < NW; ++w) pkey[w] = ld_off<uint32_t>(a.hkey, (hs << a.ksh) + 4u * w);
+      load_key(a, hs, pkey);
       prefetch_dir(a, (int32_t)hs, r);
     }
   }
@@ -315,8 +328,7 @@ struct RowCursor {
         for (int pr = 1; pr <= a.max_probe; ++pr) {
           sl = (sl + 1u) & a.hmask;
           uint32_t k[NW];
-#pragma unroll
-          for (int w = 0; w < NW; ++w) k[w] = ld_off<uint32_t>(a.hkey, (sl << a.ksh) + 4u * w);
+          load_key(a, sl, k);
           if (k[0] == kEmptyKey) break;
           if (same_key(k, key)) { found = true; break; }
         }
