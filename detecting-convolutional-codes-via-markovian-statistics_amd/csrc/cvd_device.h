@@ -135,7 +135,7 @@ constexpr int kEarlyEvery = 128;   // steps between checks (the k = 1 butterfly 
 struct ExpArgs {
   const uint32_t* filt;     // [fmask + 1][2] Bloom filter blocks over the row keys (filter_pattern)
   const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors, word 0 = kEmptyKey if empty
-  const uint32_t* hrow;     // [hcap][row_words(n)]: log P̂1[r] (f64), successor row[r] (i32, -1 = not a row)
+  const uint32_t* hrow;     // [hcap][row_words(n)]: per r, {log P̂1[r] (f64), successor row[r] (i32, -1 = not a row), pad}
   const uint32_t* drow;     // [rows][row_words(n)]: the same records dense by row id (table mode)
   const double* ltref;      // [R + 1]
   const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
@@ -228,32 +228,25 @@ __device__ __forceinline__ void fill_filter_patterns() {
 template <int NW, int R>
 struct RowCursor {
   static constexpr uint32_t RSB = 4u * row_words_c(R);   // record bytes
+  static_assert(RSB == 16u * R, "record = one 16-byte entry per received word");
   int32_t slot, pnx;
   uint32_t hs, fb, fw, fb1, fw1;   // filter block words and their patterns
   bool cand;
   double plp;
   uint32_t pkey[NW];
-  // record entries (log P̂1, successor row) of row s (dense records, table mode)
-  // or of directory slot s (a hashed lookup's hit) for word rn
-  // (the successor entries' base moves into the uniform pointer, so each address is
-  // one shift-add of the lane's word onto the record offset)
-  // (the asm keeps LLVM from deriving one address from the other with two more ops)
-  __device__ static void rec_offsets(uint32_t off, uint32_t rn, uint32_t& o_lp, uint32_t& o_nx) {
-    asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(o_lp) : "v"(rn), "v"(off));
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(o_nx) : "v"(rn), "v"(off));
+  // record entry r (log P̂1[r], successor row[r]: 16 bytes, one 12-byte load) of
+  // row s (dense records, table mode) or of directory slot s (a hashed lookup's
+  // hit) for word rn; the asm keeps the address one shift-add of the lane's word
+  // onto the record offset
+  __device__ void load_entry(const uint32_t* base, uint32_t off, uint32_t rn) {
+    uint32_t o;
+    asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o) : "v"(rn), "v"(off));
+    const uint3 v = ld_off<uint3>(base, o);
+    plp = __hiloint2double((int)v.y, (int)v.x);
+    pnx = (int32_t)v.z;
   }
-  __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
-    uint32_t o_lp, o_nx;
-    rec_offsets((uint32_t)s * RSB, rn, o_lp, o_nx);
-    plp = ld_off<double>(a.drow, o_lp);
-    pnx = ld_off<int32_t>(reinterpret_cast<const char*>(a.drow) + 8u * R, o_nx);
-  }
-  __device__ void prefetch_dir(const ExpArgs& a, int32_t s, uint32_t rn) {
-    uint32_t o_lp, o_nx;
-    rec_offsets((uint32_t)s << a.rsh, rn, o_lp, o_nx);
-    plp = ld_off<double>(a.hrow, o_lp);
-    pnx = ld_off<int32_t>(reinterpret_cast<const char*>(a.hrow) + 8u * R, o_nx);
-  }
+  __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) { load_entry(a.drow, (uint32_t)s * RSB, rn); }
+  __device__ void prefetch_dir(const ExpArgs& a, int32_t s, uint32_t rn) { load_entry(a.hrow, (uint32_t)s << a.rsh, rn); }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
     // (CVD_ABL & 4: a pattern no filter word passes, so no lane ever becomes a candidate)
     slot = a.slot0; hs = 0u; fb = (CVD_ABL & 4) ? 1u : 0u; fw = 0u; fb1 = 0u; fw1 = 0u; cand = false;
@@ -333,8 +326,9 @@ struct RowCursor {
           if (same_key(k, key)) { found = true; break; }
         }
         if (found) {
-          lpv = ld_off<double>(a.hrow, (sl << a.rsh) + 8u * r);
-          ns = ld_off<int32_t>(a.hrow, (sl << a.rsh) + 4u * (2u * R + r));
+          const uint3 v = ld_off<uint3>(a.hrow, (sl << a.rsh) + 16u * r);
+          lpv = __hiloint2double((int)v.y, (int)v.x);
+          ns = (int32_t)v.z;
         }
       }
     }

@@ -537,11 +537,14 @@ void build_hash(cvd_model& Mo) {
     slot_of[(size_t)i] = (int64_t)slot;
   }
   parallel_for(Mo.n_rows, [&](int64_t i, int) {
+    // entry r = 16 bytes {log P̂1[r] (f64), successor row (i32, -1: none), 0}: one
+    // 12-byte device load per step
     uint32_t* dw = Mo.h_drow.data() + (size_t)i * Mo.h_rsw;
-    std::memcpy(dw, Mo.logp1.data() + (size_t)i * R, sizeof(double) * R);
     for (int r = 0; r < R; ++r) {
+      std::memcpy(dw + 4 * r, Mo.logp1.data() + (size_t)i * R + r, sizeof(double));
       const int64_t j = Mo.row_next[(size_t)i * R + r];
-      dw[2 * R + r] = (uint32_t)(j >= 0 ? (int32_t)j : -1);
+      dw[4 * r + 2] = (uint32_t)(j >= 0 ? (int32_t)j : -1);
+      dw[4 * r + 3] = 0u;
     }
     uint32_t* hw = interleave ? Mo.h_key.data() + (size_t)slot_of[(size_t)i] * ssw + nw
                               : Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw;

@@ -37,7 +37,7 @@ struct cvd_model {
   std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector, word 0 = kEmptyKey if empty
   int32_t h_rsw = 0;              // row record stride in dwords (row_words)
   int32_t h_ssw = 0;              // directory slot stride in dwords: nw, or (CVD_SLOT_IL) key + record in one slot
-  std::vector<uint32_t> h_row;    // [hcap][h_rsw]: log P̂1[r] (2^n f64), successor row[r] (2^n i32, -1: none)
+  std::vector<uint32_t> h_row;    // [hcap][h_rsw]: per r, 16 B {log P̂1[r] (f64), successor row[r] (i32, -1: none), 0}
   std::vector<uint32_t> h_drow;   // [n_rows][h_rsw]: the same records dense by row id (table mode)
   int32_t slot0 = 0;              // row of D_0 = 0 (always 0)
   std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
