@@ -194,15 +194,17 @@ __device__ __forceinline__ T ld_off(const void* base, uint32_t byte_off) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
-// Bloom-filter bit patterns (cvd_keys.h filter_pattern) in LDS: one table per
-// workgroup, filled at kernel start (fill_filter_patterns + __syncthreads).
-__device__ __forceinline__ uint32_t* filter_patterns_lds() {
-  __shared__ uint32_t s_pat[cvd::kFilterPatterns];
+// Bloom-filter bit-pattern pairs (cvd_keys.h filter_pattern / filter_pattern_hi)
+// in LDS, 8 bytes each: one table per workgroup, filled at kernel start
+// (fill_filter_patterns + __syncthreads).
+__device__ __forceinline__ uint2* filter_patterns_lds() {
+  __shared__ uint2 s_pat[cvd::kFilterPatterns];
   return s_pat;
 }
 __device__ __forceinline__ void fill_filter_patterns() {
-  uint32_t* t = filter_patterns_lds();
-  for (int i = threadIdx.x; i < cvd::kFilterPatterns; i += blockDim.x) t[i] = cvd::filter_pattern((unsigned)i);
+  uint2* t = filter_patterns_lds();
+  for (int i = threadIdx.x; i < cvd::kFilterPatterns; i += blockDim.x)
+    t[i] = make_uint2(cvd::filter_pattern((unsigned)i), cvd::filter_pattern_hi((unsigned)i));
 }
 
 // Ablation knobs for timing studies only (profiles/ab_k1b.py --no-check; results
@@ -348,11 +350,12 @@ struct RowCursor {
       uint32_t ph, pl;
       cvd::key_hash_less<kLo>(key_in, NW, kLo + (hi ? 1u : 0u), ph, pl);   // = key_hash(key_in - kmu8)
       // byte offsets straight from the hash bits (cvd_keys.h: filter block (pl >> 3) & fmask,
-      // patterns (ph >> 2) and (ph >> 14) & (kFilterPatterns - 1))
+      // pattern pair (ph >> 3) & (kFilterPatterns - 1)): one AND each
       hs = ph & a.hmask;
-      const char* pt = reinterpret_cast<const char*>(filter_patterns_lds());
-      fb = *reinterpret_cast<const uint32_t*>(pt + (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 2)));
-      fb1 = *reinterpret_cast<const uint32_t*>(pt + ((ph >> 12) & (uint32_t)((cvd::kFilterPatterns - 1) << 2)));
+      const uint2 pp = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(filter_patterns_lds()) +
+                                                       (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 3)));
+      fb = pp.x;
+      fb1 = pp.y;
       const uint2 f = ld_off<uint2>(a.filt, pl & a.fmask4);
       fw = f.x;
       fw1 = f.y;

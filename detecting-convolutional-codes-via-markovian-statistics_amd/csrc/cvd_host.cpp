@@ -528,7 +528,7 @@ void build_hash(cvd_model& Mo) {
     const uint32_t ph = phs[(size_t)i], pl = pls[(size_t)i];
     const size_t fb = (size_t)filter_block_index(pl, (uint32_t)(fcap / 2 - 1));
     Mo.h_filt[2 * fb] |= filter_pattern(filter_pattern_index(ph));
-    Mo.h_filt[2 * fb + 1] |= filter_pattern(filter_pattern_index_hi(ph));
+    Mo.h_filt[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph));
     uint64_t slot = ph & (uint64_t)(cap - 1);
     int probe = 0;
     while (Mo.h_key[slot * ssw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }

@@ -37,9 +37,9 @@ CVD_HD unsigned long long mul_wide(unsigned a, unsigned b) { return (unsigned lo
 // accumulate fold, one v_mad_u64_u32 per key word with a distinct odd
 // multiplier, then one finalising 32x32->64 product p = x * C of the folded
 // word.  The home slot is ph & hmask, the filter block (pl >> 3) & bmask and the
-// filter patterns bits 2..13 and 14..25 of ph (the device takes the block and
-// the low pattern as byte offsets, pl & (bmask << 3) and ph & ((kFilterPatterns
-// - 1) << 2): one AND each).  Quality only affects speed (probe lengths, filter false positives),
+// filter pattern pair (ph >> 3) & (kFilterPatterns - 1) (the device takes both as
+// byte offsets, pl & (bmask << 3) and ph & ((kFilterPatterns - 1) << 3): one AND
+// each).  Quality only affects speed (probe lengths, filter false positives),
 // never results.
 CVD_HD void key_hash(const unsigned* w, int nw, unsigned& ph, unsigned& pl) {
   unsigned long long acc = 0x9E3779B97F4A7C15ull ^ (unsigned)nw;
@@ -77,13 +77,13 @@ CVD_HD void key_hash_less(const unsigned* w, int nw, unsigned c, unsigned& ph, u
 // Blocked Bloom filter over the row keys (explicit path): one 64-bit block (two
 // 32-bit words) per key, a pattern of three bits in each word.  A lookup of a
 // state that is not a row (most lookups at p >= 0.05 and for every H2 sequence)
-// ends on this one L2-resident 8-byte load.  The patterns come from a table of
-// kFilterPatterns three-bit words indexed by bits 2..13 (low word) and 14..25
-// (high word) of ph (the device keeps it in LDS: one LDS read per word instead
-// of the shifts and ors of three bit positions).  Two words with three bits each
-// pass a non-row ~10x less often than one word at the same filter size (p = 0.2,
-// ~1.9 rows per 32-bit word: ~0.4% -> ~0.04%), and every false positive is a
-// directory line read.
+// ends on this one L2-resident 8-byte load.  The pattern pair comes from a table
+// of kFilterPatterns entries indexed by bits 3..14 of ph (the device keeps it in
+// LDS as 64-bit entries: one AND gives the byte offset, one LDS read the pair,
+// instead of the shifts and ors of six bit positions).  Two words with three
+// bits each pass a non-row ~10x less often than one word at the same filter size
+// (p = 0.2, ~1.9 rows per 32-bit word: ~0.4% -> ~0.04%), and every false
+// positive is a directory line read.
 constexpr int kFilterPatBits = 12, kFilterPatterns = 1 << kFilterPatBits;
 CVD_HD unsigned filter_pattern(unsigned i) {
   unsigned x = (i + 1u) * 0x9E3779B1u;
@@ -96,8 +96,9 @@ CVD_HD unsigned filter_pattern(unsigned i) {
   while (b2 == b0 || b2 == b1) b2 = (b2 + 1u) & 31u;
   return (1u << b0) | (1u << b1) | (1u << b2);
 }
-CVD_HD unsigned filter_pattern_index(unsigned ph) { return (ph >> 2) & (unsigned)(kFilterPatterns - 1); }
-CVD_HD unsigned filter_pattern_index_hi(unsigned ph) { return (ph >> 14) & (unsigned)(kFilterPatterns - 1); }
+// pattern pair i: low word filter_pattern(i), high word filter_pattern(i + kFilterPatterns)
+CVD_HD unsigned filter_pattern_hi(unsigned i) { return filter_pattern(i + (unsigned)kFilterPatterns); }
+CVD_HD unsigned filter_pattern_index(unsigned ph) { return (ph >> 3) & (unsigned)(kFilterPatterns - 1); }
 // block index (words 2b, 2b + 1); bmask = blocks - 1 (the device takes the
 // block's byte offset as pl & (bmask << 3))
 CVD_HD unsigned filter_block_index(unsigned pl, unsigned bmask) { return (pl >> 3) & bmask; }
