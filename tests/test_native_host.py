@@ -142,6 +142,20 @@ def test_sparse_model_m6(pkg):
     assert inf["logp1_unseen"] == math.log(1.0 / inf["S"])
 
 
+def test_directory_sizing(pkg, monkeypatch):
+    """Explicit-path directory (csrc/cvd_host.cpp build_hash): a power of two at load
+    <= 1/16 by default; CVD_DIR_LOAD_LOG2=s sets load <= 2^-s (read at model build)."""
+    taps = [[[1, 0, 1, 1, 0, 1, 1]], [[1, 1, 1, 1, 0, 0, 1]]]
+    code = pkg.Code(taps, 6, 1, 2)
+    inf = pkg.Model(code, 0.05, 20000, 200, 1.0, 7, enum_cap=20000).info()
+    cap, rows = inf["hash_capacity"], inf["n_rows"]
+    assert cap & (cap - 1) == 0 and 16 * rows <= cap < 32 * rows
+    monkeypatch.setenv("CVD_DIR_LOAD_LOG2", "1")
+    inf2 = pkg.Model(code, 0.05, 20000, 200, 1.0, 7, enum_cap=20000).info()
+    assert inf2["n_rows"] == rows and 2 * rows <= inf2["hash_capacity"] < 4 * rows
+    assert inf2["max_probe"] >= inf["max_probe"]
+
+
 @pytest.mark.parametrize("name,kernel", [("m6_133_171", 3), ("m3_demo", 3), ("m2_75", 2), ("r23_m4", 1)])
 def test_explicit_kernel_selection(pkg, golden, name, kernel):
     """The explicit path's kernel: butterfly (k = 1, n = 2, standard butterflies,
