@@ -75,7 +75,14 @@ def parse():
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse the multi-rank path")
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="m6", choices=["m6", "m2", "r23_m4"])
+    ap.add_argument("--config", default="m6", choices=["m6", "m2", "r23_m4", "c4"],
+                    help="m6 (headline, BASELINE configs[2]), m2 (configs[1]), r23_m4 (configs[3]), c4 "
+                         "(configs[4]: the m6 pair over the N-sweep x p-grid, a fixed total of trials sharded "
+                         "over the ranks, every step of every trial, one count all_reduce)")
+    ap.add_argument("--c4-trials", type=float, default=1e8,
+                    help="c4: total trials over all ranks and grid points (BASELINE configs[4]: 1e8), split "
+                         "evenly over the (N, p) grid points like the reference's num_iter per point")
+    ap.add_argument("--c4-N", default="1000,10000,100000,1000000", help="c4: the N grid (Pd_plotter.py:196)")
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None, help="trials per GPU per step")
     ap.add_argument("--learn-len", type=int, default=1_000_000,
@@ -155,6 +162,8 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    if a.config == "c4":
+        return run_c4(a, pkg, world, rank, local, dist)
     cc = pkg.CONFIG_CODES[a.config]
     k, n, m = cc["k"], cc["n"], cc["m"]
     N = a.N if a.N is not None else {"m6": 100_000, "m2": 10_000, "r23_m4": 100_000}[a.config]
@@ -322,11 +331,22 @@ def main():
         with open(a.pmc_traffic) as f:
             pmc = json.load(f)
         if (pmc.get("config"), pmc.get("batch"), pmc.get("N"), pmc.get("detector", "markov")) != \
-                (a.config, B, N, a.detector):
-            pmc = None
+                (a.config, B, N, a.detector) or sorted(pmc.get("per_p", {})) != sorted(str(p) for p in p_grid):
+            pmc = None   # counters of another workload (or of a single-p diagnostic run)
     valu = None
+    traffic_by_p, gen_pmc = None, None
     if pmc is not None:
-        traffic = pmc.get("detector_fetch_bytes_per_launch")
+        traffic = pmc.get("detector_fetch_bytes_per_launch")   # launch-weighted mean over the sweep
+        traffic_by_p = {p: {"fetch_bytes": e["fetch_bytes"], "fetch_x_algorithmic": e["fetch_x_algorithmic"],
+                            "fetch_raw_x_algorithmic": e["fetch_raw_x_algorithmic"],
+                            "valu_insts_per_wave_step": e["VALU_insts_per_wave_step"],
+                            "vmem_rd_insts_per_wave_step": e["VMEM_RD_insts_per_wave_step"]}
+                        for p, e in pmc["per_p"].items()}
+        g = pmc.get("generator") or {}
+        if g.get("counters_per_launch"):
+            gen_pmc = {k: g[k] for k in ("kernel", "fetch_bytes_raw", "VALU_insts_per_wave", "VALU_insts_per_stream_word",
+                                         "SALU_insts_per_stream_word", "busy_frac_of_wave_cycles",
+                                         "wait_any_frac_of_wave_cycles") if k in g}
         traffic_src = os.path.relpath(a.pmc_traffic, ROOT) + " (" + pmc.get("traffic_basis", "rocprofv3 FETCH_SIZE") + ")"
         ipws = pmc.get("VALU_insts_per_wave_step")
         if ipws:
@@ -364,7 +384,8 @@ def main():
         "config": {"name": a.config, "detector": a.detector,
                    "workload": f"{a.config} pair {cc['gen1']} vs {cc['gen2']}, N={N}, p-sweep {p_grid}, "
                                f"one p per step", "N": N, "p_grid": p_grid,
-                   "trials_per_step_per_gpu": B, "model": info["kind"] and "sparse(learned)" or "dense",
+                   "trials_per_step_per_gpu": B, "k": k, "n": n, "m": m,
+                   "model": info["kind"] and "sparse(learned)" or "dense",
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "roofline": {"bound": "valu" if valu else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -373,6 +394,8 @@ def main():
                                 else pkg.KERNEL_NAMES[info["explicit_kernel"]] if info["kind"]
                                 else "detect_table_kernel (enumerated state automaton)"),
                      "traffic_source": traffic_src,
+                     "traffic_x_algorithmic": (traffic / alg_bytes) if traffic else None,
+                     "traffic_by_p": traffic_by_p,
                      "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms,
                      "valu": valu},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
@@ -380,6 +403,7 @@ def main():
                        "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
                        "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
                        "detector_ms_steps": det_each,
+                       "generator_pmc": gen_pmc,
                        "per_p": per_p},
     }
     if early_out is not None:
@@ -389,6 +413,110 @@ def main():
         out["cpu_baseline"], _ = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds, host)
         out["pd_match_vs_cpu"] = pd_match(pkg, det, cc, a.config, k, n, m, a.seed, a.cpu_seconds, host)
         out["c0_demo"] = c0_demo(pkg, host)
+    print(json.dumps(out, default=_json_default), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def run_c4(a, pkg, world, rank, local, dist):
+    """BASELINE.json configs[4]: the m = 6 pair over N in {1e3, 1e4, 1e5, 1e6} x the
+    p grid, `--c4-trials` trials in total (1e8), the same number at every (N, p) grid
+    point (the reference's num_iter per point, Pd_plotter.py:196-233: N outer, p
+    inner).  Rank r of W takes the contiguous global trial ids [r T/W, (r+1) T/W) of
+    every point; every step of every trial runs (cvd_mc_run: generator + detector,
+    no early decision); ONE all_reduce of the [nN, np, 2] count tensor at the end.
+    The counts depend on the global trial ids only, so they are the same for any W."""
+    import numpy as np
+    import torch
+    cc = pkg.CONFIG_CODES["m6"]
+    k, n, m = cc["k"], cc["n"], cc["m"]
+    Ns = [int(float(x)) for x in a.c4_N.split(",") if x]
+    p_grid = P_GRID if a.p is None else [a.p]
+    npt = len(Ns) * len(p_grid)
+    T = max(world, int(a.c4_trials) // npt)        # trials per grid point (all ranks)
+    lo, hi = rank * T // world, (rank + 1) * T // world
+    det = pkg.Detector(k, n, m, cc["gen1"], device=local)
+    t_setup = time.perf_counter()
+    models = dict(zip(p_grid, det.prepare_models(p_grid, a.learn_len, 200, 1.0, a.seed)))
+    t_setup = time.perf_counter() - t_setup
+    free, _ = torch.cuda.mem_get_info(det.device)
+    budget = min(int(free * 0.6), 131 << 30)         # one batch's streams (the bench's 131 GB at N = 1e5)
+
+    def batch_of(N):
+        b = det.default_batch(N, hi - lo, budget)
+        return max(1, b)
+
+    counts = torch.zeros((len(Ns), len(p_grid), 2), dtype=torch.int64, device=det.device)
+    # warmup: one small launch per p (smallest N) at trial ids far from the timed ones
+    for p in p_grid:
+        det.run_trials(models[p], cc["gen1"], cc["gen2"], min(Ns), p, a.seed, 1 << 44, (1 << 44) + 1024,
+                       batch=1024, counts=torch.zeros(2, dtype=torch.int64, device=det.device))
+    torch.cuda.synchronize()
+    per_n_s = []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for iN, N in enumerate(Ns):
+        tn = time.perf_counter()
+        B = batch_of(N)
+        for ip, p in enumerate(p_grid):
+            det.run_trials(models[p], cc["gen1"], cc["gen2"], N, p, a.seed, lo, hi, batch=B,
+                           counts=counts[iN, ip], early_decision=False)
+        torch.cuda.synchronize()
+        per_n_s.append(time.perf_counter() - tn)
+        print(json.dumps({"c4_progress": {"rank": rank, "N": N, "seconds": per_n_s[-1]}}), file=sys.stderr,
+              flush=True)
+    if dist:
+        dist.all_reduce(counts)                  # the one collective: success counts over RCCL
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dev = det.device if a.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed] + per_n_s, device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, per_n_s = float(t[0]), [float(x) for x in t[1:].tolist()]
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    c = counts.cpu().numpy()
+    total = T * npt
+    per_N = {str(N): {"trials": T * len(p_grid), "seconds": per_n_s[i], "trials_per_s": T * len(p_grid) / per_n_s[i],
+                      "seq_steps_per_s": 2 * T * len(p_grid) * N / per_n_s[i],
+                      "batch_per_rank": batch_of(N),
+                      "per_p": {str(p): {"h1_successes": int(c[i, j, 0]), "h2_successes": int(c[i, j, 1]),
+                                         "Pd": float(c[i, j, 0]) / T, "Pc": float(c[i, j, 0] + c[i, j, 1]) / (2 * T)}
+                                for j, p in enumerate(p_grid)}}
+             for i, N in enumerate(Ns)}
+    out = {
+        "metric": "MC trials/sec (C4: m=6 pair, N-sweep x p-grid, fixed total trials, sharded over GPUs)",
+        "value": total / elapsed,
+        "unit": "trials/s",
+        "n_gpus": world,
+        "steps": npt,
+        "warmup": 1,
+        "ms_per_step": elapsed / npt * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u16x2 (metrics) + f64 (log-likelihood sums)",
+        "data": "synthetic: Philox4x32-10 encoder inputs and BSC(p) flips (build spec), learned P̂1",
+        "config": {"name": "c4", "workload": f"m6 pair {cc['gen1']} vs {cc['gen2']}, N in {Ns} x p {p_grid}, "
+                                             f"{T} trials per grid point ({total} total), one step = one grid point",
+                   "N_grid": Ns, "p_grid": p_grid, "trials_per_point": T, "total_trials": total,
+                   "learn_len": a.learn_len, "early_decision": False,
+                   "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
+        "per_N": per_N,
+        "counts": c.tolist(),
+        "diagnostic": {"model_setup_s": t_setup, "elapsed_s": elapsed},
+    }
+    if a.cpu_baseline and world == 1:
+        host = host_info(a.cpu_threads)
+        out["cpu_baseline"], _ = cpu_baseline(cc, k, n, m, 100_000, a.seed, a.learn_len, a.cpu_seconds, host)
     print(json.dumps(out, default=_json_default), flush=True)
     if dist:
         dist.destroy_process_group()

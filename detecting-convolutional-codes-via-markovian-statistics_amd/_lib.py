@@ -12,7 +12,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5
 DETECT_EARLY_DECISION = 0x100   # OR'ed into path: counts only, stop once every decision is certain
@@ -67,6 +67,7 @@ EXPORTS = {
     "cvd_model_info_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cvd_model_info)]),
     "cvd_model_dense_P1": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "cvd_model_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "cvd_model_taps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "cvd_model_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "cvd_model_destroy": (None, [ctypes.c_void_p]),
     "cvd_model_save": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),

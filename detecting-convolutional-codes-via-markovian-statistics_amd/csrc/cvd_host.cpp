@@ -3,7 +3,9 @@
 // tables and the explicit-path hash.  None of this is the hot path (the trial
 // loop runs in cvd_kernels.hip); it is the analogue of the reference's table
 // construction (viterbi_markov.py:118-230, Pd_plotter.py:123-169).
+#include <atomic>
 #include <chrono>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -20,6 +22,9 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "../../include/cvd.h"
 #include "cvd_internal.h"
@@ -640,6 +645,16 @@ bool cvd::explicit_supported(int m, int k, int n) {
 }
 
 namespace {
+// The GPU chain refused the model (a shape or chain length it does not take, or
+// too little device memory for its scratch): the host chain, which gives the
+// same model bit for bit, runs instead (recorded in LearnStats).  Any other
+// device error is returned as is.
+bool device_refused(int rc, LearnStats* stats) {
+  if (rc != CVD_E_UNSUPPORTED && rc != CVD_E_CAPACITY) return false;
+  if (stats) stats->host_fallback = 1;
+  return true;
+}
+
 // cvd_model_create / cvd_model_create_device: the learning chain on the host
 // (device < 0) or on a GPU (cvd_learn.hip; same outputs), everything else shared.
 int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, void* stream, cvd_model** out,
@@ -692,10 +707,14 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
     const int64_t L = prm->learn_len < 0 ? std::max<int64_t>(5000, 200 * S) : prm->learn_len;
     Mo->learn_len_eff = L;
     std::vector<int64_t> cnt((size_t)S * R, 0);
+    bool on_host = true;
     if (device >= 0 && L >= 1) {   // (an empty chain, L = 0, has nothing to run)
       rc = device_learn_dense(Mo->dec, next, S, L, prm->learn_burn, seed, prm->p, device, stream, cnt, stats);
-      if (rc) return rc;
-    } else {
+      on_host = device_refused(rc, stats);
+      if (rc && !on_host) return rc;
+      if (on_host) cnt.assign((size_t)S * R, 0);
+    }
+    if (on_host) {
       HostStream hs(Mo->dec, T, seed, kLearnTag, 0, prm->p, true);
       int64_t i = 0;   // D_0 = 0 is BFS index 0
       for (int64_t t = 0; t < L; ++t) {
@@ -744,20 +763,27 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
     std::vector<uint8_t> keys;
     StateMap map(M, &keys);
     std::vector<int64_t> cnt;
+    bool on_host = true;
     if (device >= 0 && L >= 1) {
       // the chain on the GPU: rows in first-visit order + counts; the host map is
       // rebuilt from the rows (insertion order = row order) for the successors
       std::vector<uint8_t> rows;
       int64_t Sd = 0;
       rc = device_learn_sparse(Mo->dec, L, prm->learn_burn, seed, prm->p, device, stream, rows, cnt, Sd, stats);
-      if (rc) return rc;
-      map.reserve(Sd);
-      bool ins;
-      for (int64_t s = 0; s < Sd; ++s) {
-        map.insert(rows.data() + (size_t)s * M, ins);
-        if (!ins) { set_error("GPU learning: duplicate row key"); return CVD_E_STATE; }
+      on_host = device_refused(rc, stats);
+      if (rc && !on_host) return rc;
+      if (!on_host) {
+        map.reserve(Sd);
+        bool ins;
+        for (int64_t s = 0; s < Sd; ++s) {
+          map.insert(rows.data() + (size_t)s * M, ins);
+          if (!ins) { set_error("GPU learning: duplicate row key"); return CVD_E_STATE; }
+        }
+      } else {
+        cnt.clear();
       }
-    } else {
+    }
+    if (on_host) {
       map.reserve(std::min<int64_t>(L + 1, (int64_t)1 << 26));
       std::vector<uint8_t> D((size_t)M, 0), Dn((size_t)M);
       const HostStep step(T);
@@ -858,7 +884,12 @@ struct Reader {
 extern "C" int cvd_model_save(const cvd_model* Mo, const char* path) {
   CVD_TRY
   if (!Mo || !path) { set_error("null argument"); return CVD_E_INVALID; }
-  const std::string tmp = std::string(path) + ".tmp";
+  // a tmp name of this process and thread (ranks sharing a cache directory save
+  // the same model at once), then an atomic rename over the target
+  static std::atomic<uint64_t> serial{0};
+  const std::string tmp = std::string(path) + ".tmp." + std::to_string((long long)getpid()) + "." +
+                          std::to_string((unsigned long long)std::hash<std::thread::id>()(std::this_thread::get_id())) +
+                          "." + std::to_string((unsigned long long)serial++);
   FILE* f = std::fopen(tmp.c_str(), "wb");
   if (!f) { set_error(std::string("cannot write ") + tmp); return CVD_E_INVALID; }
   Writer w{f};
@@ -873,6 +904,9 @@ extern "C" int cvd_model_save(const cvd_model* Mo, const char* path) {
   const bool ok = w.ok && std::fclose(f) == 0;
   if (!ok || std::rename(tmp.c_str(), path) != 0) {
     std::remove(tmp.c_str());
+    // another writer's rename may have won the race: its file is the same model
+    struct stat sb;
+    if (ok && stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) return CVD_OK;
     set_error(std::string("cannot write ") + path);
     return CVD_E_INVALID;
   }
@@ -905,9 +939,27 @@ extern "C" int cvd_model_load(const char* path, cvd_model** out) {
   const CodeDesc& d = Mo->dec;
   const bool shape_ok = d.k >= 1 && d.k <= kMaxK && d.n >= 1 && d.n <= kMaxN && d.m >= 1 && d.m <= kMaxM;
   const size_t M = shape_ok ? (size_t)1 << d.m : 0, R = shape_ok ? (size_t)1 << d.n : 0;
-  if (!r.ok || !shape_ok || Mo->n_rows < 1 || Mo->keys.size() != (size_t)Mo->n_rows * M ||
-      Mo->logp1.size() != (size_t)Mo->n_rows * R || Mo->row_next.size() != (size_t)Mo->n_rows * R ||
-      Mo->ltref.size() != R + 1) {
+  bool valid = r.ok && shape_ok && (Mo->kind == 0 || Mo->kind == 1) && Mo->n_rows >= 1 &&
+               Mo->n_rows < ((int64_t)1 << 31) && Mo->keys.size() == (size_t)Mo->n_rows * M &&
+               Mo->logp1.size() == (size_t)Mo->n_rows * R && Mo->row_next.size() == (size_t)Mo->n_rows * R &&
+               Mo->ltref.size() == R + 1;
+  // dense models: S rows, one 32-bit record and one row sum per (row, word) / row,
+  // every record's successor a row; sparse: S = rows.  Successors must be rows or
+  // -1, and every metric byte a nibble: the device tables are built from these
+  // without further checks
+  if (valid && Mo->kind == 0)
+    valid = Mo->S == Mo->n_rows && Mo->rec.size() == (size_t)Mo->n_rows * R &&
+            Mo->rowsum.size() == (size_t)Mo->n_rows;
+  if (valid && Mo->kind == 1) valid = Mo->S == Mo->n_rows;
+  for (size_t i = 0; valid && i < Mo->row_next.size(); ++i)
+    valid = Mo->row_next[i] >= -1 && Mo->row_next[i] < Mo->n_rows && (Mo->kind == 1 || Mo->row_next[i] >= 0);
+  for (size_t i = 0; valid && i < Mo->rec.size(); ++i)
+    valid = (int64_t)(Mo->rec[i] >> 4) < Mo->n_rows && (Mo->rec[i] & 15u) >= 1 && (Mo->rec[i] & 15u) <= R;
+  for (size_t i = 0; valid && i < Mo->keys.size(); ++i) valid = Mo->keys[i] < 15;
+  for (size_t i = 0; valid && i < Mo->p1_nz.size(); ++i)
+    valid = Mo->p1_nz[i].row >= 0 && Mo->p1_nz[i].row < Mo->n_rows && Mo->p1_nz[i].col >= 0 &&
+            Mo->p1_nz[i].col < Mo->n_rows;
+  if (!valid) {
     set_error(std::string("corrupt model file: ") + path);
     return CVD_E_INVALID;
   }
@@ -939,6 +991,8 @@ extern "C" int cvd_model_create_device(const cvd_code* dec, const cvd_learn_para
     stats_out[2] = (double)st.fix_passes;
     stats_out[3] = (double)st.sequential_blocks;
     stats_out[4] = (double)st.hash_attempts;
+    stats_out[5] = (double)st.host_fallback;
+    stats_out[6] = st.sequential_seconds;
   }
   return rc;
 }
@@ -991,6 +1045,17 @@ extern "C" int cvd_model_jit_status(const cvd_model* Mo, char* msg_out, int64_t 
   }
   if (Mo->device < 0 || !Mo->k1b_ok || Mo->hcap == 0) return 0;   // not applicable
   return Mo->rtc_fn ? 1 : -1;
+}
+
+extern "C" int cvd_model_taps(const cvd_model* Mo, uint8_t* taps_out, int64_t len) {
+  if (!Mo || !taps_out) { set_error("null argument"); return CVD_E_INVALID; }
+  const CodeDesc& d = Mo->dec;
+  const int L = d.m + 1;
+  if (len != (int64_t)d.n * d.k * L) { set_error("taps buffer size must be n*k*(m+1)"); return CVD_E_INVALID; }
+  for (int j = 0; j < d.n; ++j)
+    for (int i = 0; i < d.k; ++i)
+      for (int t = 0; t < L; ++t) taps_out[(j * d.k + i) * L + t] = (uint8_t)((d.gmask[j * d.k + i] >> t) & 1u);
+  return CVD_OK;
 }
 
 extern "C" int cvd_model_upload(cvd_model* Mo, int device) {

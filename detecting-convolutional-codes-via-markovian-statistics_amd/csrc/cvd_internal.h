@@ -108,6 +108,8 @@ struct LearnStats {
   int64_t sequential_blocks = 0;   // blocks re-run one by one (cascading mismatches)
   int64_t hash_attempts = 0;       // sort passes (>1: a 64-bit key-hash collision was seen)
   double seconds = 0.0;
+  double sequential_seconds = 0.0; // time of the sequential tail (0 unless it ran)
+  int64_t host_fallback = 0;       // 1: the GPU chain refused (shape, length, device memory), host chain ran
 };
 // sparse model: rows = distinct D_0..D_L in first-visit order (keys_out [S][2^m]
 // bytes), cnt_out[S][2^n] = transitions over t in [burn, L)

@@ -32,6 +32,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -47,7 +48,7 @@ using namespace cvd;
     hipError_t e_ = (x);                                                                  \
     if (e_ != hipSuccess) {                                                               \
       set_error(std::string("HIP error '") + hipGetErrorString(e_) + "' at " #x);          \
-      return CVD_E_HIP;                                                                   \
+      return e_ == hipErrorOutOfMemory ? CVD_E_CAPACITY : CVD_E_HIP;                      \
     }                                                                                     \
   } while (0)
 
@@ -61,6 +62,8 @@ struct ChainArgs {
   const int32_t* list;     // blocks to run (nullptr: block = thread index)
   int64_t nlist;
   const uint32_t* start;   // exact start state of list[i] (nullptr: speculative from D = 0)
+  int32_t seq;             // 1: one lane runs list[0..nlist) in order, each block from its
+                           // predecessor's end (the bounded sequential tail of run_chain)
   uint32_t* states;        // sparse: [(L+1)][NW] keys; dense: [(L+1)] indices
   uint32_t* ends;          // [nblocks][NW or 1]: state at the block's end
   const int32_t* next;     // dense: [S][R] automaton
@@ -123,26 +126,33 @@ __global__ __launch_bounds__(kLB) void chain_sparse_kernel(ChainArgs a) {
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kLB + threadIdx.x;
   const int64_t nb = a.list ? a.nlist : a.nblocks;
-  if (i >= nb) return;
-  const int64_t b = a.list ? a.list[i] : i;
-  const int64_t s0 = b * a.blen, e0 = min(s0 + a.blen, a.L);
-  uint8_t D[M];
-  int64_t t;
-  if (a.start) {
-    unpack_key<m>(a.start + i * NW, D);
-    t = s0;
-  } else {
+  if (i >= nb || (a.seq && i > 0)) return;
+  // seq: this lane walks every listed block in order; block list[j] starts from
+  // the end state the lane has just written for list[j] - 1
+  for (int64_t j = a.seq ? 0 : i; j < (a.seq ? nb : i + 1); ++j) {
+    const int64_t b = a.list ? a.list[j] : j;
+    const int64_t s0 = b * a.blen, e0 = min(s0 + a.blen, a.L);
+    uint8_t D[M];
+    int64_t t;
+    if (a.seq) {
+      unpack_key<m>(a.ends + (size_t)(b - 1) * NW, D);
+      t = s0;
+    } else if (a.start) {
+      unpack_key<m>(a.start + j * NW, D);
+      t = s0;
+    } else {
 #pragma unroll
-    for (int x = 0; x < M; ++x) D[x] = 0;
-    t = max((int64_t)0, s0 - a.warm);
-    for (; t < s0; ++t) step_vec<m, k>(D, s_bm + word_at(a.r, t, n) * (M * K));
+      for (int x = 0; x < M; ++x) D[x] = 0;
+      t = max((int64_t)0, s0 - a.warm);
+      for (; t < s0; ++t) step_vec<m, k>(D, s_bm + word_at(a.r, t, n) * (M * K));
+    }
+    for (; t < e0; ++t) {
+      pack_key<m>(D, a.states + (size_t)t * NW);
+      step_vec<m, k>(D, s_bm + word_at(a.r, t, n) * (M * K));
+    }
+    pack_key<m>(D, a.ends + (size_t)b * NW);
+    if (e0 == a.L) pack_key<m>(D, a.states + (size_t)a.L * NW);
   }
-  for (; t < e0; ++t) {
-    pack_key<m>(D, a.states + (size_t)t * NW);
-    step_vec<m, k>(D, s_bm + word_at(a.r, t, n) * (M * K));
-  }
-  pack_key<m>(D, a.ends + (size_t)b * NW);
-  if (e0 == a.L) pack_key<m>(D, a.states + (size_t)a.L * NW);
 }
 
 template <int n>
@@ -150,25 +160,30 @@ __global__ __launch_bounds__(kLB) void chain_dense_kernel(ChainArgs a) {
   constexpr int R = 1 << n;
   const int64_t i = (int64_t)blockIdx.x * kLB + threadIdx.x;
   const int64_t nb = a.list ? a.nlist : a.nblocks;
-  if (i >= nb) return;
-  const int64_t b = a.list ? a.list[i] : i;
-  const int64_t s0 = b * a.blen, e0 = min(s0 + a.blen, a.L);
-  int32_t s;
-  int64_t t;
-  if (a.start) {
-    s = (int32_t)a.start[i];
-    t = s0;
-  } else {
-    s = 0;   // D_0 = 0 is BFS index 0
-    t = max((int64_t)0, s0 - a.warm);
-    for (; t < s0; ++t) s = a.next[(size_t)s * R + word_at(a.r, t, n)];
+  if (i >= nb || (a.seq && i > 0)) return;
+  for (int64_t j = a.seq ? 0 : i; j < (a.seq ? nb : i + 1); ++j) {
+    const int64_t b = a.list ? a.list[j] : j;
+    const int64_t s0 = b * a.blen, e0 = min(s0 + a.blen, a.L);
+    int32_t s;
+    int64_t t;
+    if (a.seq) {
+      s = (int32_t)a.ends[b - 1];
+      t = s0;
+    } else if (a.start) {
+      s = (int32_t)a.start[j];
+      t = s0;
+    } else {
+      s = 0;   // D_0 = 0 is BFS index 0
+      t = max((int64_t)0, s0 - a.warm);
+      for (; t < s0; ++t) s = a.next[(size_t)s * R + word_at(a.r, t, n)];
+    }
+    for (; t < e0; ++t) {
+      a.states[t] = (uint32_t)s;
+      s = a.next[(size_t)s * R + word_at(a.r, t, n)];
+    }
+    a.ends[b] = (uint32_t)s;
+    if (e0 == a.L) a.states[a.L] = (uint32_t)s;
   }
-  for (; t < e0; ++t) {
-    a.states[t] = (uint32_t)s;
-    s = a.next[(size_t)s * R + word_at(a.r, t, n)];
-  }
-  a.ends[b] = (uint32_t)s;
-  if (e0 == a.L) a.states[a.L] = (uint32_t)s;
 }
 
 // bad[b] = block b's start state differs from block b-1's end state (b >= 1)
@@ -297,7 +312,7 @@ int64_t env_int(const char* name, int64_t def) {
 int run_chain(ChainArgs a, int nw, void (*kern)(ChainArgs), size_t lds, hipStream_t st, Scratch& sc,
               LearnStats* stats) {
   a.nblocks = (a.L + a.blen - 1) / a.blen;
-  a.list = nullptr; a.start = nullptr; a.nlist = 0;
+  a.list = nullptr; a.start = nullptr; a.nlist = 0; a.seq = 0;
   hipLaunchKernelGGL(kern, dim3(grid_of(a.nblocks)), dim3(kLB), lds, st, a);
   LHIP(hipGetLastError());
   uint8_t* bad = nullptr;
@@ -308,6 +323,8 @@ int run_chain(ChainArgs a, int nw, void (*kern)(ChainArgs), size_t lds, hipStrea
   LHIP(sc.alloc(d_start, (size_t)a.nblocks * nw));
   std::vector<uint8_t> h_bad((size_t)a.nblocks);
   std::vector<int32_t> list;
+  // parallel re-run passes before the sequential tail (CVD_LEARN_MAX_PASSES: tests)
+  const int64_t max_passes = std::max<int64_t>(0, env_int("CVD_LEARN_MAX_PASSES", 8));
   for (int pass = 0;; ++pass) {
     hipLaunchKernelGGL(verify_kernel, dim3(grid_of(a.nblocks)), dim3(kLB), 0, st, a.states, a.ends, a.blen,
                        a.nblocks, nw, bad);
@@ -325,22 +342,24 @@ int run_chain(ChainArgs a, int nw, void (*kern)(ChainArgs), size_t lds, hipStrea
     // each pass makes the first failing block exact (its predecessor is); to stay
     // bounded when mismatches cascade, re-run from the first failing block to the
     // end once the passes exceed a few
-    if (pass >= 8) {
+    if (pass >= max_passes) {
+      // sequential tail: ONE launch in which one lane re-runs every block from the
+      // first failing one to the end, in order, each from its predecessor's end
+      // (bounded: one kernel, L - first * blen steps; timed in LearnStats)
+      const auto t0 = std::chrono::steady_clock::now();
       const int32_t first = list.front();
       list.clear();
       for (int64_t b = first; b < a.nblocks; ++b) list.push_back((int32_t)b);
-      // sequentially: one block at a time from the exact predecessor
       LHIP(hipMemcpyAsync(d_list, list.data(), list.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
-      for (size_t j = 0; j < list.size(); ++j) {
-        hipLaunchKernelGGL(gather_starts_kernel, dim3(1), dim3(kLB), 0, st, a.ends, d_list + j, (int64_t)1, nw,
-                           d_start);
-        ChainArgs f = a;
-        f.list = d_list + j; f.nlist = 1; f.start = d_start;
-        hipLaunchKernelGGL(kern, dim3(1), dim3(kLB), lds, st, f);
-        LHIP(hipGetLastError());
-      }
+      ChainArgs f = a;
+      f.list = d_list; f.nlist = (int64_t)list.size(); f.start = nullptr; f.seq = 1;
+      hipLaunchKernelGGL(kern, dim3(1), dim3(kLB), lds, st, f);
+      LHIP(hipGetLastError());
       LHIP(hipStreamSynchronize(st));
-      if (stats) stats->sequential_blocks = (int64_t)list.size();
+      if (stats) {
+        stats->sequential_blocks = (int64_t)list.size();
+        stats->sequential_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      }
       return CVD_OK;
     }
     LHIP(hipMemcpyAsync(d_list, list.data(), list.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
@@ -387,7 +406,7 @@ int cvd::device_learn_sparse(const CodeDesc& dec, int64_t L, int64_t burn, uint6
                              int64_t& S_out, LearnStats* stats) {
   const int m = dec.m, k = dec.k, n = dec.n, M = 1 << m, R = 1 << n, nw = M >= 8 ? M / 8 : 1;
   if (!pick_sparse(m, k, n)) { set_error("GPU learning: unsupported code shape"); return CVD_E_UNSUPPORTED; }
-  if (L < 1 || L >= ((int64_t)1 << 31)) { set_error("GPU learning: learn_len must be in [1, 2^31)"); return CVD_E_INVALID; }
+  if (L < 1 || L >= ((int64_t)1 << 31)) { set_error("GPU learning: learn_len must be in [1, 2^31)"); return CVD_E_UNSUPPORTED; }
   DevGuard guard;
   LHIP(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;
@@ -476,7 +495,7 @@ int cvd::device_learn_dense(const CodeDesc& dec, const std::vector<int32_t>& nex
                             std::vector<int64_t>& cnt_out, LearnStats* stats) {
   const int n = dec.n, R = 1 << n;
   if (n < 1 || n > 3) { set_error("GPU learning: n must be 1..3"); return CVD_E_UNSUPPORTED; }
-  if (L < 1 || L >= ((int64_t)1 << 31)) { set_error("GPU learning: learn_len must be in [1, 2^31)"); return CVD_E_INVALID; }
+  if (L < 1 || L >= ((int64_t)1 << 31)) { set_error("GPU learning: learn_len must be in [1, 2^31)"); return CVD_E_UNSUPPORTED; }
   DevGuard guard;
   LHIP(hipSetDevice(device));
   hipStream_t st = (hipStream_t)stream;

@@ -106,8 +106,11 @@ class Model:
                 h = ctypes.c_void_p()
                 if self._lib.cvd_model_load(path.encode(), ctypes.byref(h)) == 0:
                     self._h = h
-                    self.from_cache = True
-                    return
+                    if self.code_key() == dec.key:
+                        self.from_cache = True
+                        return
+                    self._lib.cvd_model_destroy(h)   # a stale file under this key: learn again
+                    self._h = None
         prm = _lib.cvd_learn_params(float(p), -1 if learn_len is None else int(learn_len),
                                     int(learn_burn), float(laplace), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                     int(enum_cap), int(default_learn_len))
@@ -115,14 +118,18 @@ class Model:
         if learn_device is None:
             _lib.check(self._lib.cvd_model_create(dec.c, ctypes.byref(prm), ctypes.byref(h)))
         else:
-            st = (ctypes.c_double * 5)()
+            st = (ctypes.c_double * 7)()
             _lib.check(self._lib.cvd_model_create_device(dec.c, ctypes.byref(prm), int(learn_device), None,
                                                          ctypes.byref(h), ctypes.cast(st, ctypes.c_void_p)))
             self.learn_stats = dict(zip(("seconds", "mismatched_blocks", "fix_passes", "sequential_blocks",
-                                         "hash_attempts"), list(st)))
+                                         "hash_attempts", "host_fallback", "sequential_seconds"), list(st)))
         self._h = h
         if path is not None:
-            _lib.check(self._lib.cvd_model_save(self._h, path.encode()))
+            # best effort: a cache that cannot be written (read-only or full disk) never
+            # fails the run; concurrent writers are safe (unique tmp + atomic rename)
+            if self._lib.cvd_model_save(self._h, path.encode()) != 0:
+                warnings.warn(f"model cache not written ({path}): "
+                              f"{self._lib.cvd_last_error().decode(errors='replace')}", RuntimeWarning, stacklevel=2)
 
     def save(self, path):
         _lib.check(self._lib.cvd_model_save(self._h, os.fspath(path).encode()))
@@ -136,7 +143,18 @@ class Model:
         _lib.check(self._lib.cvd_model_load(os.fspath(path).encode(), ctypes.byref(h)))
         self._h = h
         self.p = float("nan")
+        if self.code_key() != dec.key:
+            raise _lib.CvdError(f"model file {os.fspath(path)} was learned for another code "
+                                f"(k, n, m, taps) than {dec!r}")
         return self
+
+    def code_key(self):
+        """(k, n, m, taps bytes) of the model's decoder, comparable with Code.key."""
+        inf = self.info()
+        k, n, m = inf["k"], inf["n"], inf["m"]
+        taps = np.zeros(n * k * (m + 1), np.uint8)
+        _lib.check(self._lib.cvd_model_taps(self._h, taps.ctypes.data, taps.size))
+        return (k, n, m, taps.tobytes())
 
     @property
     def handle(self):

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 4
+#define CVD_ABI_VERSION 5
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -114,8 +114,11 @@ int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm, cvd_model
 /* The same model with the learning chain (Pd_plotter.py:143-163) run on GPU `device`
  * (parallel in time: speculative blocks verified at their boundaries, first visits
  * by a radix sort of key hashes; see cvd_learn.hip).  Bit-identical to
- * cvd_model_create.  stats_out (nullable) [5]: seconds, mismatched speculative
- * blocks, re-run passes, blocks re-run sequentially, hash/sort attempts.
+ * cvd_model_create.  stats_out (nullable) [7]: seconds, mismatched speculative
+ * blocks, re-run passes, blocks re-run sequentially, hash/sort attempts,
+ * host fallback (1: the GPU chain refused the code shape, the chain length
+ * (>= 2^31) or ran out of device memory for its scratch, and the host chain
+ * built the model -- identical results), seconds of the sequential tail.
  * Synchronous; `stream` orders the device work (NULL = default stream). */
 int cvd_model_create_device(const cvd_code* dec, const cvd_learn_params* prm, int32_t device, void* stream,
                             cvd_model** out, double* stats_out);
@@ -124,6 +127,9 @@ int cvd_model_info_get(const cvd_model* model, cvd_model_info* info);
 int cvd_model_dense_P1(const cvd_model* model, double* P_out, int64_t S);
 /* Per-row tables (host copies): logP1[row*2^n + r]; keys[row][2^m] metric bytes. */
 int cvd_model_rows(const cvd_model* model, double* logp1_out, uint8_t* keys_out, int64_t n_rows);
+/* The decoder code of a model (e.g. one loaded from a file): taps_out receives
+ * [n][k][m+1] delay-ordered taps (cvd_code layout); len = its size in bytes. */
+int cvd_model_taps(const cvd_model* model, uint8_t* taps_out, int64_t len);
 int cvd_model_upload(cvd_model* model, int device);
 /* The code-specialised detector kernel (CVD_KERNEL_BUTTERFLY_RTC) of an uploaded
  * model: 1 = built, -1 = unavailable (msg_out receives the compiler's reason, the

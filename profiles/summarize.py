@@ -36,8 +36,10 @@ def main(src, name):
         w.writerows(rows)
     bench = json.load(open(os.path.join(src, "bench_trace.json")))
     json.dump(bench, open(os.path.join(dst, "bench_under_rocprof.json"), "w"), indent=1)
-    agg, cnt = {}, {}
-    for i, f in enumerate(sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")))):
+    # counters per dispatch: detector launch i of a pass is bench step i, so its p is
+    # p_grid[i % len(p_grid)] (--warmup 0, no CPU legs: only the timed launches run)
+    det_rows, gen_rows = {}, {}
+    for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
         keep = [r for r in csv.DictReader(open(f)) if is_det(r["Kernel_Name"]) or is_gen(r["Kernel_Name"])]
         tag = os.path.basename(os.path.dirname(f))
         with open(os.path.join(dst, f"{tag}.csv"), "w", newline="") as g:
@@ -45,48 +47,100 @@ def main(src, name):
             w.writeheader()
             w.writerows(keep)
         for r in keep:
+            tgt = det_rows if is_det(r["Kernel_Name"]) else gen_rows
+            d = tgt.setdefault(tag, {}).setdefault(int(r["Dispatch_Id"]), {})
+            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
             if is_det(r["Kernel_Name"]):
-                k = r["Counter_Name"]
-                agg[k] = agg.get(k, 0.0) + float(r["Counter_Value"])
-                cnt[k] = cnt.get(k, 0) + 1
-    per = {k: agg[k] / cnt[k] for k in agg}
+                d["_kernel"] = r["Kernel_Name"]
     cfg = bench["config"]
+    p_grid = cfg.get("p_grid", [None])
     B, N = cfg["trials_per_step_per_gpu"], cfg["N"]
-    waves = per.get("SQ_WAVES", 2 * B / 64)
-    kernel_cycles = per.get("GRBM_GUI_ACTIVE", 0.0) / 8   # GRBM_GUI_ACTIVE sums the 8 XCDs
-    out = {
-        "kernel": bench["roofline"]["kernel"],
-        "workload": f"bench.py --steps 2 --warmup 0 (p = 0.01, 0.02), {B} trials x 2 sequences, N = {N}",
-        "source": "rocprofv3 --pmc, one counter group per pass (profiles/collect.sh), averaged per detector launch",
-        "FETCH_SIZE_kB_per_launch": per.get("FETCH_SIZE"),
-        "WRITE_SIZE_kB_per_launch": per.get("WRITE_SIZE"),
-        "detector_fetch_bytes_per_launch_raw": per.get("FETCH_SIZE", 0.0) * 1024,
+    alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+    by_p = {}
+    for tag, disp in det_rows.items():
+        for i, did in enumerate(sorted(disp)):
+            e = by_p.setdefault(str(p_grid[i % len(p_grid)]), {"counters": {}, "launches": {}})
+            for k, v in disp[did].items():
+                if k.startswith("_"):
+                    continue
+                e["counters"][k] = e["counters"].get(k, 0.0) + v
+                e["launches"][k] = e["launches"].get(k, 0) + 1
+    ms_by_p = bench["diagnostic"].get("detector_ms_by_p", {})
+
+    def derive(c, ms=None):
+        waves = c.get("SQ_WAVES", 2 * B / 64)
+        raw = c.get("FETCH_SIZE", 0.0) * 1024
         # The guide's x2 (FETCH_SIZE = half of a 16-B/lane streaming read) applies to the
         # stream chunks only: they are the algorithmic bytes, read once as 16-B lane loads,
         # so they appear as algorithmic / 2 in the raw count.  The rest (filter words,
         # directory lines, row records: 8-128 B random reads, uncalibrated) is taken raw.
-        "detector_fetch_bytes_per_launch": per.get("FETCH_SIZE", 0.0) * 1024 + min(
-            per.get("FETCH_SIZE", 0.0) * 1024, bench["roofline"]["algorithmic_bytes_per_launch"] / 2),
-        "traffic_basis": "rocprofv3 FETCH_SIZE; the 16-B/lane stream reads x2 (MI355X_MICROARCH.md), the random reads raw",
+        corr = raw + min(raw, alg / 2)
+        kc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8   # GRBM_GUI_ACTIVE sums the 8 XCDs
+        out = {"fetch_bytes_raw": raw, "fetch_bytes": corr, "fetch_x_algorithmic": corr / alg,
+               "fetch_raw_x_algorithmic": raw / alg,
+               "VALU_insts_per_wave_step": c.get("SQ_INSTS_VALU", 0.0) / (waves * N),
+               "SALU_insts_per_wave_step": c.get("SQ_INSTS_SALU", 0.0) / (waves * N),
+               "VMEM_RD_insts_per_wave_step": c.get("SQ_INSTS_VMEM_RD", 0.0) / (waves * N),
+               "wait_any_frac_of_wave_cycles": c.get("SQ_WAIT_ANY", 0.0) / max(1.0, c.get("SQ_WAVE_CYCLES", 1.0)),
+               "active_valu_frac_of_wave_cycles": c.get("SQ_ACTIVE_INST_VALU", 0.0) / max(1.0, c.get("SQ_WAVE_CYCLES", 1.0)),
+               "kernel_cycles": kc}
+        if ms is not None:
+            out["detector_ms_live"] = ms
+        return out
+
+    per_p = {}
+    for p, e in by_p.items():
+        c = {k: e["counters"][k] / e["launches"][k] for k in e["counters"]}
+        per_p[p] = dict(derive(c, ms_by_p.get(p)), counters_per_launch=c)
+    # launch-weighted sweep mean: every p of the sweep is one launch of the same batch
+    keys = set().union(*[set(v["counters_per_launch"]) for v in per_p.values()]) if per_p else set()
+    per = {k: sum(v["counters_per_launch"].get(k, 0.0) for v in per_p.values()) / max(1, len(per_p)) for k in keys}
+    sweep = derive(per)
+    waves = per.get("SQ_WAVES", 2 * B / 64)
+    kernel_cycles = sweep["kernel_cycles"]
+    gen = {}
+    for tag, disp in gen_rows.items():
+        for did, d in disp.items():
+            for k, v in d.items():
+                gen.setdefault(k, []).append(v)
+    gen_per = {k: sum(v) / len(v) for k, v in gen.items()}
+    out = {
+        "kernel": bench["roofline"]["kernel"],
+        "workload": f"bench.py --config {cfg.get('name')} --steps {len(p_grid)} --warmup 0: one launch per p of "
+                    f"{p_grid}, {B} trials x 2 sequences, N = {N}",
+        "source": "rocprofv3 --pmc, one counter group per pass (profiles/collect_sweep.sh), per detector launch",
+        "per_p": per_p,
+        "sweep_mean": sweep,
+        "detector_fetch_bytes_per_launch_raw": sweep["fetch_bytes_raw"],
+        "detector_fetch_bytes_per_launch": sweep["fetch_bytes"],
+        "traffic_basis": "rocprofv3 FETCH_SIZE, launch-weighted mean over the p sweep; the 16-B/lane stream "
+                         "reads x2 (MI355X_MICROARCH.md), the random reads raw",
         "correction": "x2 on the stream part only (algorithmic bytes / 2 of the raw count: 16-B/lane chunk loads, read "
                       "once); the row-table traffic is 8-128 B random accesses, which the guide leaves uncalibrated, "
                       "taken raw",
-        "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
+        "algorithmic_bytes_per_launch": alg,
         "SQ_INSTS_VALU_per_launch": per.get("SQ_INSTS_VALU"),
-        "VALU_insts_per_wave_step": per.get("SQ_INSTS_VALU", 0.0) / (waves * N),
-        "SALU_insts_per_wave_step": per.get("SQ_INSTS_SALU", 0.0) / (waves * N),
-        "VMEM_RD_insts_per_wave_step": per.get("SQ_INSTS_VMEM_RD", 0.0) / (waves * N),
+        "VALU_insts_per_wave_step": sweep["VALU_insts_per_wave_step"],
+        "SALU_insts_per_wave_step": sweep["SALU_insts_per_wave_step"],
+        "VMEM_RD_insts_per_wave_step": sweep["VMEM_RD_insts_per_wave_step"],
         "SQ_WAVES": waves,
         "GRBM_GUI_ACTIVE": per.get("GRBM_GUI_ACTIVE"),
         "kernel_cycles": kernel_cycles,
-        # VALU issue capacity: 1024 SIMDs, one wave64 instruction per 2 cycles (plain VOP2
-        # add/sub/logic/16-bit) or 4 cycles (VOP3/VOP3P/shifts: the packed ACS ops),
-        # measured on MI355X (.scratch microbenchmarks); the hot loop averages
-        # ~3.5 issue cycles per VALU instruction (static mix of the JIT kernel)
-        "valu_issue_frac_est": per.get("SQ_INSTS_VALU", 0.0) * 3.5 / (1024 * max(1.0, kernel_cycles)),
         "wait_inst_any_frac_of_wave_cycles": per.get("SQ_WAIT_INST_ANY", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
         "active_valu_frac_of_wave_cycles": per.get("SQ_ACTIVE_INST_VALU", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
         "counters_per_launch": per,
+        "generator": {
+            "kernel": "gen_fast_kernel (encoder + BSC noise, two launches per step: H1, H2)",
+            "counters_per_launch": gen_per,
+            "fetch_bytes_raw": gen_per.get("FETCH_SIZE", 0.0) * 1024,
+            "VALU_insts_per_wave": gen_per.get("SQ_INSTS_VALU", 0.0) / max(1.0, gen_per.get("SQ_WAVES", 1.0)),
+            "VALU_insts_per_stream_word": gen_per.get("SQ_INSTS_VALU", 0.0) * 64 / max(1.0, B * ((N * cfg.get("n", 2) + 31) // 32)),
+            "SALU_insts_per_stream_word": gen_per.get("SQ_INSTS_SALU", 0.0) * 64 / max(1.0, B * ((N * cfg.get("n", 2) + 31) // 32)),
+            "busy_frac_of_wave_cycles": gen_per.get("SQ_ACTIVE_INST_ANY", 0.0) / max(1.0, gen_per.get("SQ_WAVE_CYCLES", 1.0)),
+            "wait_any_frac_of_wave_cycles": gen_per.get("SQ_WAIT_ANY", 0.0) / max(1.0, gen_per.get("SQ_WAVE_CYCLES", 1.0)),
+            "note": "one launch writes B sequences (H1 or H2) of ceil(N n / 32) words; VALU per stream word counts "
+                    "wave-instructions x 64 lanes / words written",
+        },
         "config": cfg.get("name", "m6"),
         "detector": cfg.get("detector", "markov"),
         "batch": B,
@@ -115,9 +169,14 @@ def main(src, name):
                                      "issue cost per class (profiles/valu_issue_cycles.json)")
         out["valu_mix_by_class_per_step"] = by_class
         out["valu_issue_cycle_frac"] = per.get("SQ_INSTS_VALU", 0.0) * avg / (1024 * max(1.0, kernel_cycles))
+        for e in out["per_p"].values():
+            c = e["counters_per_launch"]
+            e["valu_issue_cycle_frac"] = c.get("SQ_INSTS_VALU", 0.0) * avg / (1024 * max(1.0, e["kernel_cycles"]))
     fn = f"pmc_{out['detector']}_{out['config']}.json"
     json.dump(out, open(os.path.join(ROOT, "profiles", fn), "w"), indent=1)
-    print(json.dumps({k: v for k, v in out.items() if k != "counters_per_launch"}, indent=1))
+    print(json.dumps({k: v for k, v in out.items() if k not in ("counters_per_launch", "per_p")}, indent=1))
+    for p, e in sorted(out["per_p"].items(), key=lambda x: float(x[0]) if x[0] != "None" else 0):
+        print(p, {k: round(v, 3) if isinstance(v, float) else v for k, v in e.items() if k != "counters_per_launch"})
 
 
 if __name__ == "__main__":

@@ -102,3 +102,26 @@ def test_bench_launches_its_own_ranks(tmp_path):
     bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *common],
                          timeout=120, capture_output=True, text=True, env=dict(env, WORLD_SIZE="1"))
     assert bad.returncode != 0
+
+
+def test_bench_c4_counts_rank_invariant():
+    """`bench.py --config c4` (BASELINE configs[4]: the m6 pair over an N grid x the p grid,
+    a fixed total of trials split evenly over the grid points, every step of every trial,
+    one count all_reduce): two ranks (gloo, both on the one GPU) give exactly the counts of
+    one rank, since the streams are keyed by the global trial id."""
+    env = dict(os.environ, CVD_BENCH_ONE_DEVICE="1")
+    env.pop("WORLD_SIZE", None)
+    common = ["--config", "c4", "--c4-trials", "4800", "--c4-N", "1000,10000", "--learn-len", "100000",
+              "--cpu-baseline", "0"]
+    two = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                          *common], timeout=300, capture_output=True, text=True, env=env)
+    assert two.returncode == 0, two.stderr[-4000:]
+    one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *common],
+                         timeout=300, capture_output=True, text=True, env=env)
+    assert one.returncode == 0, one.stderr[-4000:]
+    j2 = json.loads([ln for ln in two.stdout.splitlines() if ln.startswith("{")][-1])
+    j1 = json.loads([ln for ln in one.stdout.splitlines() if ln.startswith("{")][-1])
+    assert j2["n_gpus"] == 2 and j1["n_gpus"] == 1 and j1["scaling"] == "strong"
+    assert j1["config"]["total_trials"] == 4800 and set(j1["per_N"]) == {"1000", "10000"}
+    assert j2["counts"] == j1["counts"]
+    assert sum(c[0] + c[1] for row in j1["counts"] for c in row) > 0

@@ -87,3 +87,29 @@ def test_detector_learns_on_gpu_by_default(pkg, dev):
     det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
     mod = det.model(0.05, 200_000, 200, 1.0, 3)
     assert mod.learn_stats is not None and mod.learn_stats["hash_attempts"] >= 1
+
+
+def test_sequential_tail_is_one_bounded_launch(pkg, dev, monkeypatch):
+    """CVD_LEARN_MAX_PASSES=0: the first failing block and everything after it re-run in
+    ONE launch, one lane walking the blocks in order (no per-block launches); the model
+    is still the host chain's and the tail's time is reported."""
+    monkeypatch.setenv("CVD_LEARN_WARM", "0")
+    monkeypatch.setenv("CVD_LEARN_BLOCK", "256")
+    monkeypatch.setenv("CVD_LEARN_MAX_PASSES", "0")
+    cc = pkg.CONFIG_CODES["m6"]
+    _, gpu = _pair(pkg, cc["gen1"], 6, 1, 2, 0.05, 60_000)
+    st = gpu.learn_stats
+    assert st["mismatched_blocks"] > 0 and st["sequential_blocks"] > 0 and st["sequential_seconds"] > 0.0
+    _, gpu = _pair(pkg, pkg.CONFIG_CODES["m2"]["gen1"], 2, 1, 2, 0.05, None)
+
+
+def test_gpu_learning_falls_back_to_host_chain(pkg, dev):
+    """A dense code the GPU chain does not take (n = 4 > 3) still builds through the
+    device path: the host chain runs (host_fallback = 1), same model as cvd_model_create."""
+    taps = [[[1, 1, 1]], [[1, 0, 1]], [[1, 1, 0]], [[0, 1, 1]]]   # rate 1/4, m = 2
+    host, gpu = _pair(pkg, taps, 2, 1, 4, 0.05, None)
+    assert gpu.learn_stats["host_fallback"] == 1.0
+    det = pkg.Detector(1, 4, 2, taps, device=0)   # the default (GPU-learning) Detector path
+    assert det.model(0.05).learn_stats["host_fallback"] == 1.0
+    _, gpu = _pair(pkg, pkg.CONFIG_CODES["m2"]["gen1"], 2, 1, 2, 0.05, None)
+    assert gpu.learn_stats["host_fallback"] == 0.0

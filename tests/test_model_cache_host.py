@@ -57,3 +57,62 @@ def test_load_rejects_foreign_file(pkg, tmp_path):
     code = pkg.Code([[[1, 1, 1]], [[1, 0, 1]]], 2, 1, 2)
     with pytest.raises(pkg.CvdError):
         pkg.Model.load(code, bad)
+
+
+def test_concurrent_saves_of_one_key(pkg, golden, tmp_path):
+    """Ranks sharing a cache directory save the same model at once: every save
+    succeeds (unique tmp names, atomic rename) and the file loads."""
+    import threading
+    z, meta = golden
+    k, n, m, taps = code_of(meta, "m2_75")
+    code = pkg.Code(taps, m, k, n)
+    a = pkg.Model(code, 0.05, None, 200, 1.0, 9)
+    path = tmp_path / "same.bin"
+    errs = []
+
+    def save():
+        try:
+            for _ in range(20):
+                a.save(path)
+        except Exception as e:   # pragma: no cover - the failure being tested for
+            errs.append(e)
+
+    th = [threading.Thread(target=save) for _ in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
+    assert [f for f in os.listdir(tmp_path)] == ["same.bin"]   # no tmp files left behind
+    _same(a, pkg.Model.load(code, path))
+
+
+def test_unwritable_cache_warns_instead_of_failing(pkg, golden, tmp_path, monkeypatch):
+    z, meta = golden
+    k, n, m, taps = code_of(meta, "m2_75")
+    code = pkg.Code(taps, m, k, n)
+    monkeypatch.setenv("CVD_MODEL_CACHE", str(tmp_path))
+    key = pkg.detector.model_cache_key(code, 0.05, None, 200, 1.0, 4, pkg.detector.DEFAULT_ENUM_CAP,
+                                       pkg.detector.DEFAULT_SPARSE_LEARN_LEN)
+    (tmp_path / key).mkdir()          # the cache file's name is taken by a directory
+    with pytest.warns(RuntimeWarning, match="model cache not written"):
+        mod = pkg.Model(code, 0.05, None, 200, 1.0, 4)
+    assert not mod.from_cache and mod.info()["S"] == 31
+
+
+def test_load_rejects_corrupt_successor_and_foreign_code(pkg, golden, tmp_path):
+    z, meta = golden
+    k, n, m, taps = code_of(meta, "m6_133_171")
+    code = pkg.Code(taps, m, k, n)
+    a = pkg.Model(code, 0.05, 20000, 200, 1.0, 3)
+    path = tmp_path / "m.bin"
+    a.save(path)
+    raw = bytearray(path.read_bytes())
+    raw[-8:] = np.int64(a.info()["n_rows"] + 5).tobytes()   # last successor entry out of range
+    bad = tmp_path / "bad.bin"
+    bad.write_bytes(bytes(raw))
+    with pytest.raises(pkg.CvdError, match="corrupt"):
+        pkg.Model.load(code, bad)
+    other = pkg.Code([[[1, 1, 1, 1, 0, 0, 1]], [[1, 0, 1, 1, 0, 1, 1]]], 6, 1, 2)
+    with pytest.raises(pkg.CvdError, match="another code"):
+        pkg.Model.load(other, path)
