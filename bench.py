@@ -577,10 +577,15 @@ def cpu_baseline(cc, k, n, m, N, seed, learn_len, seconds, host):
     t0 = time.perf_counter()
     c_smp, _ = mod.run_trials(c1, c2, N, p, seed, 0, ntr, nthreads=threads)
     dt = time.perf_counter() - t0
+    basis = ("threads = OMP_NUM_THREADS (the GPU box's CPU share for one GPU, set by the pool; the "
+             f"process affinity allows {host['affinity_cpus']} CPUs of the host, which the pool's rules "
+             "reserve for other jobs)") if host["omp_num_threads_env"] else \
+        f"threads = every CPU in this process's affinity ({host['affinity_cpus']})"
     return {"value": ntr / dt, "unit": "trials/s", "cores": threads, "kind": "port",
+            "per_core_value": ntr / dt / threads,
             "sample": f"{ntr} trials (H1+H2, N={N}) at p={p} of the headline sweep, C oracle "
                       f"(oracle/cvd_oracle.c, OpenMP), {threads} threads, {dt:.1f} s",
-            "seconds": dt, "host": host}, [int(x) for x in c_smp]
+            "basis": basis, "seconds": dt, "host": host}, [int(x) for x in c_smp]
 
 
 def pd_match(pkg, det, cc, config, k, n, m, seed, seconds, host):

@@ -10,6 +10,7 @@ from .detector import (  # noqa: F401
     DEFAULTS, N_SPECTRUM_BY_M, Detector, Model, run_experiment, learn_P1_empirical,
     enumerate_markov_states_allzero, build_trellis, branch_output_and_next_state,
     viterbi_metric_step, simulate_markov_sequence, log_likelihood_ratio, grid_tag, LEARN_TAG,
+    enumerate_states_device,
 )
 from .parity import (  # noqa: F401
     parse_poly_token, build_parity_system, nullspace_mod2, parity_vector_to_equation, parity_vectors,

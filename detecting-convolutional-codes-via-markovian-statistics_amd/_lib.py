@@ -59,6 +59,10 @@ EXPORTS = {
                                        ctypes.c_void_p]),
     "cvd_enumerate": (ctypes.c_int, [ctypes.POINTER(cvd_code), ctypes.c_int64,
                                      ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p, ctypes.c_void_p]),
+    "cvd_enumerate_device": (ctypes.c_int, [ctypes.POINTER(cvd_code), ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                            ctypes.c_void_p]),
     "cvd_model_create": (ctypes.c_int, [ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_learn_params),
                                         ctypes.POINTER(ctypes.c_void_p)]),
     "cvd_model_create_device": (ctypes.c_int, [ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_learn_params),

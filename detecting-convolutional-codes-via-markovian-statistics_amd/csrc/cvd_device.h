@@ -215,6 +215,9 @@ __device__ __forceinline__ void fill_filter_patterns() {
 #ifndef CVD_ABL
 #define CVD_ABL 0
 #endif
+#ifndef CVD_K1B_CMP64
+#define CVD_K1B_CMP64 1
+#endif
 
 // Lookup of the P̂1 row of the current metric state.  A learned row's record
 // holds the row of its successor for every received word, so a sequence that
@@ -300,6 +303,29 @@ struct RowCursor {
     asm volatile("" : "+v"(d));
     return d == 0u;
   }
+  // stored (canonical) key x == lazy key y - kmu8?  y's words are x + kmu8 with no
+  // carry out of any nibble (nibbles <= 14 + 2), so as 64-bit word pairs y = x + K
+  // exactly, K = kmu8 * (2^32 + 1): one 64-bit add and one 64-bit compare per pair
+  // (v_lshl_add_u64, v_cmp_eq_u64) instead of a subtract, a xor and an or per word
+  __device__ static bool same_key_lazy(const uint32_t (&x)[NW], const uint32_t (&y)[NW], uint32_t kmu8) {
+#if CVD_K1B_CMP64
+    if constexpr (NW % 2 == 0) {
+      const uint64_t K = (uint64_t)kmu8 * 0x100000001ull;
+      bool eq = true;
+#pragma unroll
+      for (int i = 0; i < NW / 2; ++i) {
+        const uint64_t xi = ((uint64_t)x[2 * i + 1] << 32) | x[2 * i];
+        const uint64_t yi = ((uint64_t)y[2 * i + 1] << 32) | y[2 * i];
+        eq = eq && (xi + K == yi);
+      }
+      return eq;
+    }
+#endif
+    uint32_t key[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) key[w] = y[w] - kmu8;
+    return same_key(x, key);
+  }
   // log P̂1(row(D_{t-1}), r); afterwards `slot` describes row(D_t)
   // kmu8: the stored key is the canonical key + kmu8 in every nibble (lazy
   // normalisation, CVD_K1B_LAZYKEY); subtracted only where the key is compared
@@ -311,12 +337,12 @@ struct RowCursor {
     if (slot >= 0) {
       lpv = plp; ns = pnx;
     } else if (cand) {
-      uint32_t key[NW];
-#pragma unroll
-      for (int w = 0; w < NW; ++w) key[w] = key_in[w] - kmu8;
-      if (same_key(pkey, key)) {
+      if (same_key_lazy(pkey, key_in, kmu8)) {
         lpv = plp; ns = (CVD_ABL & 16) ? -2 : pnx;
       } else if (pkey[0] != kEmptyKey) {
+        uint32_t key[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) key[w] = key_in[w] - kmu8;
         // home slot holds another row: linear probing up to an empty slot
         uint32_t sl = hs;
         bool found = false;

@@ -430,6 +430,33 @@ def enumerate_markov_states_allzero(generator_matrix, m, k, n, cap=DEFAULT_ENUM_
     return states, transitions, all_r
 
 
+def enumerate_states_device(generator_matrix, m, k, n, device=0, cap=1 << 40, mem_bytes=0, with_tables=False,
+                            max_levels=1 << 16):
+    """viterbi_markov.py:166-195 on the GPU (cvd_enumerate_device).
+
+    Returns {"S", "complete", "level_sizes", "states"?, "next"?}: complete = False when
+    the state count passed `cap` or the device memory budget, and S is then a certified
+    lower bound (distinct reachable states found).  with_tables: also the states in
+    discovery order ([S, 2^m] uint8) and next[S, 2^n] (int32, by received word)."""
+    code = as_code(generator_matrix, m, k, n)
+    lib = _lib.lib()
+    S = ctypes.c_int64()
+    nl = ctypes.c_int32()
+    lv = np.zeros(max_levels, np.int64)
+    rc = lib.cvd_enumerate_device(code.c, int(device), int(cap), int(mem_bytes), ctypes.byref(S), None, None,
+                                  lv.ctypes.data, int(max_levels), ctypes.byref(nl), None)
+    if rc not in (0, -3):
+        _lib.check(rc)
+    out = {"S": int(S.value), "complete": rc == 0, "level_sizes": lv[:min(nl.value, max_levels)].tolist()}
+    if with_tables and rc == 0:
+        st = np.zeros((S.value, 1 << m), np.uint8)
+        nx = np.zeros((S.value, 1 << n), np.int32)
+        _lib.check(lib.cvd_enumerate_device(code.c, int(device), int(S.value), int(mem_bytes), ctypes.byref(S),
+                                            st.ctypes.data, nx.ctypes.data, None, 0, ctypes.byref(nl), None))
+        out["states"], out["next"] = st, nx
+    return out
+
+
 class Trellis(dict):
     """build_trellis result (viterbi_markov.py:118-132) that also carries the code."""
 

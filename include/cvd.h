@@ -6,7 +6,8 @@
  *   ───────────────────────────────────────────────────────────────────────────   ─────────────────────
  *   viterbi_markov.py:82-106  branch_output_and_next_state                         cvd_code_tables
  *   viterbi_markov.py:139-159 viterbi_metric_step (Eq. 4-5)                        cvd_metric_step (host), cvd_trace (GPU)
- *   viterbi_markov.py:166-195 enumerate_markov_states_allzero (BFS)                cvd_enumerate
+ *   viterbi_markov.py:166-195 enumerate_markov_states_allzero (BFS)                cvd_enumerate (host),
+ *                                                                                  cvd_enumerate_device (GPU)
  *   viterbi_markov.py:202-230 + Pd_plotter.py:89-99  T(p) at p = 1/2              cvd_model_* (|Y(i,j)|/2^n, exact)
  *   Pd_plotter.py:123-169     learn_P1_empirical                                   cvd_model_create (host chain),
  *                                                                                  cvd_model_create_device (GPU chain)
@@ -108,6 +109,20 @@ int cvd_metric_step(const cvd_code* dec, const uint8_t* D_prev, int32_t r, uint8
  * Returns CVD_E_CAPACITY if more than `cap` states exist. */
 int cvd_enumerate(const cvd_code* dec, int64_t cap, int64_t* S_out,
                   uint8_t* states_out, int32_t* next_out);
+
+/* The same BFS on GPU `device` (for codes past the host
+ * BFS, (133,171) > 2e8 states): level-synchronous over a hash set in HBM, states in
+ * the reference's discovery order (a level's new states ranked by their first
+ * (parent, received word) in itertools.product order).  Same outputs as
+ * cvd_enumerate (states_out / next_out nullable), plus level_sizes[l] = states
+ * first reached after l steps (nullable, max_levels entries; n_levels_out the
+ * number of levels).  mem_bytes: device memory budget (<= 0: 90% of free).
+ * CVD_E_CAPACITY when S > cap or the budget cannot hold the search: S_out is then
+ * a certified lower bound (distinct reachable states found) and the level sizes
+ * describe the levels reached.  Synchronous. */
+int cvd_enumerate_device(const cvd_code* dec, int32_t device, int64_t cap, int64_t mem_bytes, int64_t* S_out,
+                         uint8_t* states_out, int32_t* next_out, int64_t* level_sizes, int32_t max_levels,
+                         int32_t* n_levels_out, void* stream);
 
 /* ---- model: decoder trellis + learned P̂1 + T_ref(1/2) ------------------------ */
 int cvd_model_create(const cvd_code* dec, const cvd_learn_params* prm, cvd_model** out);
