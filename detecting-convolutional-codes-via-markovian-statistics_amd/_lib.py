@@ -31,7 +31,7 @@ class cvd_learn_params(ctypes.Structure):
     _fields_ = [("p", ctypes.c_double), ("learn_len", ctypes.c_int64),
                 ("learn_burn", ctypes.c_int64), ("laplace", ctypes.c_double),
                 ("seed", ctypes.c_uint64), ("enum_cap", ctypes.c_int64),
-                ("default_learn_len", ctypes.c_int64)]
+                ("default_learn_len", ctypes.c_int64), ("laplace_states", ctypes.c_int64)]
 
 
 class cvd_model_info(ctypes.Structure):

@@ -216,7 +216,7 @@ __device__ __forceinline__ void fill_filter_patterns() {
 #define CVD_ABL 0
 #endif
 #ifndef CVD_K1B_CMP64
-#define CVD_K1B_CMP64 1
+#define CVD_K1B_CMP64 0
 #endif
 
 // Lookup of the P̂1 row of the current metric state.  A learned row's record
@@ -303,10 +303,12 @@ struct RowCursor {
     asm volatile("" : "+v"(d));
     return d == 0u;
   }
-  // stored (canonical) key x == lazy key y - kmu8?  y's words are x + kmu8 with no
-  // carry out of any nibble (nibbles <= 14 + 2), so as 64-bit word pairs y = x + K
-  // exactly, K = kmu8 * (2^32 + 1): one 64-bit add and one 64-bit compare per pair
-  // (v_lshl_add_u64, v_cmp_eq_u64) instead of a subtract, a xor and an or per word
+  // stored (canonical) key x == lazy key y - kmu8?  Default: subtract, xor and or
+  // per word.  CVD_K1B_CMP64=1: y's words are x + kmu8 with no carry out of any
+  // nibble (nibbles <= 14 + 2), so as 64-bit word pairs y = x + K exactly, K = kmu8 *
+  // (2^32 + 1): one 64-bit add and one 64-bit compare per pair.  Fewer VALU in the
+  // filter-positive block, but measured neutral (p = 0.1: 710.2 vs 709.3 ms per
+  // 655,360-trial launch, profiles/r03b/ab_cmp64.jsonl), so it stays off.
   __device__ static bool same_key_lazy(const uint32_t (&x)[NW], const uint32_t (&y)[NW], uint32_t kmu8) {
 #if CVD_K1B_CMP64
     if constexpr (NW % 2 == 0) {

@@ -700,6 +700,10 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
   pt.mark("bfs");
   std::unordered_map<int64_t, double> memo;
 
+  if (rc == CVD_OK && prm->laplace_states > 0 && prm->laplace_states != S) {
+    set_error("laplace_states: an enumerable code's Laplace denominator is its BFS state count");
+    return CVD_E_INVALID;
+  }
   if (rc == CVD_OK) {
     // ── dense model: the reference's exact semantics (Pd_plotter.py:123-169) ──
     Mo->kind = 0;
@@ -803,14 +807,21 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
     }
     pt.mark("chain");
     const HostStep step(T);
-    S = map.count;
+    const int64_t rows = map.count;
+    // Laplace denominator S * laplace (Pd_plotter.py:166-167): the visited rows (D4),
+    // or a state count the caller measured / bounded (laplace_states)
+    if (prm->laplace_states > 0 && prm->laplace_states < rows) {
+      set_error("laplace_states below the number of visited states");
+      return CVD_E_INVALID;
+    }
+    S = prm->laplace_states > 0 ? prm->laplace_states : rows;
     Mo->S = S;
-    Mo->n_rows = S;
-    Mo->logp1.assign((size_t)S * R, 0.0);
-    Mo->row_next.assign((size_t)S * R, -1);
+    Mo->n_rows = rows;
+    Mo->logp1.assign((size_t)rows * R, 0.0);
+    Mo->row_next.assign((size_t)rows * R, -1);
     // successors and P̂1 rows: independent per row (read-only map), on host threads
     std::vector<std::unordered_map<int64_t, double>> memos(32);
-    parallel_for(S, [&](int64_t s, int tid) {
+    parallel_for(rows, [&](int64_t s, int tid) {
       uint8_t nb[256];
       int64_t succ[16];
       for (int r = 0; r < R; ++r) {
@@ -950,7 +961,7 @@ extern "C" int cvd_model_load(const char* path, cvd_model** out) {
   if (valid && Mo->kind == 0)
     valid = Mo->S == Mo->n_rows && Mo->rec.size() == (size_t)Mo->n_rows * R &&
             Mo->rowsum.size() == (size_t)Mo->n_rows;
-  if (valid && Mo->kind == 1) valid = Mo->S == Mo->n_rows;
+  if (valid && Mo->kind == 1) valid = Mo->S >= Mo->n_rows;
   for (size_t i = 0; valid && i < Mo->row_next.size(); ++i)
     valid = Mo->row_next[i] >= -1 && Mo->row_next[i] < Mo->n_rows && (Mo->kind == 1 || Mo->row_next[i] >= 0);
   for (size_t i = 0; valid && i < Mo->rec.size(); ++i)

@@ -74,13 +74,16 @@ def model_cache_dir(explicit=None):
     return d
 
 
-def model_cache_key(dec, p, learn_len, learn_burn, laplace, seed, enum_cap, default_learn_len):
+def model_cache_key(dec, p, learn_len, learn_burn, laplace, seed, enum_cap, default_learn_len, laplace_states=None):
     """File name of a learned model: a hash of everything the learning depends on,
     the reference's lru_cache key (Pd_plotter.py:123-127: gens, k, n, m, p,
     learn_len, learn_burn, laplace, seed) plus this build's enumeration policy and
     stream spec."""
-    txt = repr((dec.key, float(p).hex(), learn_len, int(learn_burn), float(laplace).hex(), int(seed),
-                int(enum_cap), int(default_learn_len), _lib.ABI_VERSION, "philox4x32-10/D1-D4"))
+    key = (dec.key, float(p).hex(), learn_len, int(learn_burn), float(laplace).hex(), int(seed),
+           int(enum_cap), int(default_learn_len), _lib.ABI_VERSION, "philox4x32-10/D1-D4")
+    if laplace_states:
+        key = key + (int(laplace_states),)
+    txt = repr(key)
     return "cvdm_" + hashlib.sha256(txt.encode()).hexdigest()[:40] + ".bin"
 
 
@@ -89,9 +92,12 @@ class Model:
 
     def __init__(self, dec, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345,
                  enum_cap=DEFAULT_ENUM_CAP, default_learn_len=DEFAULT_SPARSE_LEARN_LEN, cache_dir=None,
-                 learn_device=None):
+                 learn_device=None, laplace_states=None):
         """learn_device: run the learning chain on this GPU (cvd_model_create_device,
-        bit-identical to the host chain); None: on the host (cvd_model_create)."""
+        bit-identical to the host chain); None: on the host (cvd_model_create).
+        laplace_states (non-enumerable codes): the S of the reference's Laplace
+        denominator S * laplace (Pd_plotter.py:166-167), e.g. the certified lower bound
+        enumerate_states_device gives for m = 6; None: the visited rows."""
         self.dec = dec
         self.p = float(p)
         self._lib = _lib.lib()
@@ -101,7 +107,7 @@ class Model:
         d = model_cache_dir(cache_dir)
         if d is not None:
             path = os.path.join(d, model_cache_key(dec, p, learn_len, learn_burn, laplace, seed, enum_cap,
-                                                   default_learn_len))
+                                                   default_learn_len, laplace_states))
             if os.path.exists(path):
                 h = ctypes.c_void_p()
                 if self._lib.cvd_model_load(path.encode(), ctypes.byref(h)) == 0:
@@ -113,7 +119,7 @@ class Model:
                     self._h = None
         prm = _lib.cvd_learn_params(float(p), -1 if learn_len is None else int(learn_len),
                                     int(learn_burn), float(laplace), int(seed) & 0xFFFFFFFFFFFFFFFF,
-                                    int(enum_cap), int(default_learn_len))
+                                    int(enum_cap), int(default_learn_len), int(laplace_states or 0))
         h = ctypes.c_void_p()
         if learn_device is None:
             _lib.check(self._lib.cvd_model_create(dec.c, ctypes.byref(prm), ctypes.byref(h)))
@@ -220,13 +226,14 @@ class Detector:
         self.learn_device = None if os.environ.get("CVD_LEARN_HOST", "0") not in ("", "0") else self.device.index
         self._models = OrderedDict()
 
-    def model(self, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345):
-        key = (float(p), learn_len, int(learn_burn), float(laplace), int(seed))
+    def model(self, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345, laplace_states=None):
+        key = (float(p), learn_len, int(learn_burn), float(laplace), int(seed), laplace_states)
         if key in self._models:
             self._models.move_to_end(key)
             return self._models[key]
         mod = Model(self.dec, p, learn_len, learn_burn, laplace, seed, self.enum_cap,
-                    self.default_learn_len, self.model_cache, self.learn_device).upload(self.device.index)
+                    self.default_learn_len, self.model_cache, self.learn_device,
+                    laplace_states).upload(self.device.index)
         self._models[key] = mod
         while len(self._models) > 128:
             self._models.popitem(last=False)
@@ -240,7 +247,7 @@ class Detector:
         from concurrent.futures import ThreadPoolExecutor
         keys = {}
         for p in p_list:
-            key = (float(p), learn_len, int(learn_burn), float(laplace), int(seed))
+            key = (float(p), learn_len, int(learn_burn), float(laplace), int(seed), None)
             if key not in self._models:
                 keys[key] = float(p)
         if len(keys) > 1:

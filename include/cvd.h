@@ -63,6 +63,10 @@ typedef struct cvd_learn_params {
   uint64_t seed;           /* learning-chain seed (Pd_plotter.py:70 default 12345) */
   int64_t enum_cap;        /* BFS cap; above it the model is sparse (learned states only) */
   int64_t default_learn_len; /* learn length for non-enumerable codes when learn_len < 0 */
+  int64_t laplace_states;  /* non-enumerable codes: > 0 = the S of the Laplace denominator S*laplace
+                              (Pd_plotter.py:166-167), e.g. a count or certified lower bound from
+                              cvd_enumerate_device, >= the visited rows; <= 0 = the visited rows
+                              (DESIGN.md D4).  Enumerable codes: <= 0 or the BFS count S. */
 } cvd_learn_params;
 
 typedef struct cvd_model_info {

@@ -26,7 +26,7 @@ def lib():
         L.oc_model_create.restype = ctypes.c_void_p
         L.oc_model_create.argtypes = [ctypes.POINTER(oc_code), ctypes.c_double, ctypes.c_int64,
                                       ctypes.c_int64, ctypes.c_double, ctypes.c_uint64,
-                                      ctypes.c_int64, ctypes.c_int64]
+                                      ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
         L.oc_model_S.restype = ctypes.c_int64
         L.oc_model_S.argtypes = [ctypes.c_void_p]
         L.oc_model_kind.argtypes = [ctypes.c_void_p]
@@ -59,10 +59,11 @@ class Code:
 
 class Model:
     def __init__(self, dec, p, learn_len=None, learn_burn=200, laplace=1.0, seed=12345,
-                 enum_cap=500_000, sparse_default_len=1_000_000):
+                 enum_cap=500_000, sparse_default_len=1_000_000, laplace_states=0):
         self.dec = dec
         self.h = lib().oc_model_create(ctypes.byref(dec.c), p, -1 if learn_len is None else learn_len,
-                                       learn_burn, laplace, seed, enum_cap, sparse_default_len)
+                                       learn_burn, laplace, seed, enum_cap, sparse_default_len,
+                                       int(laplace_states or 0))
 
     @property
     def S(self):

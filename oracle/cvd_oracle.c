@@ -230,8 +230,11 @@ static int oc_bfs(const Tabs* T, int64_t cap, Index* I, int32_t** next_out) {
   return 0;
 }
 
+/* S_lap > 0 (non-enumerable codes): the S of the Laplace denominator S*lam
+ * (Pd:166-167) instead of the number of visited rows -- the product's
+ * cvd_learn_params.laplace_states, restated */
 void* oc_model_create(const oc_code* dec, double p, int64_t learn_len, int64_t burn, double lam,
-                      uint64_t seed, int64_t enum_cap, int64_t sparse_default_len) {
+                      uint64_t seed, int64_t enum_cap, int64_t sparse_default_len, int64_t S_lap) {
   Model* Mo = calloc(1, sizeof(Model));
   make_tabs(dec, &Mo->T);
   const Tabs* T = &Mo->T;
@@ -295,11 +298,12 @@ void* oc_model_create(const oc_code* dec, double p, int64_t learn_len, int64_t b
   }
   /* P = (counts + laplace) / rowsum  (Pd:166-167), logs as in Pd:114-115 */
   const int64_t S = Mo->S;
+  const int64_t SL = (Mo->kind == 1 && S_lap > 0) ? S_lap : S;   /* Laplace denominator's S */
   Mo->logp1 = malloc(sizeof(double) * (size_t)S * R);
   for (int64_t s = 0; s < S; ++s) {
     int64_t rs = 0;
     for (int r = 0; r < R; ++r) rs += cnt[s * R + r];
-    const double rowsum = (double)rs + (double)S * lam;
+    const double rowsum = (double)rs + (double)SL * lam;
     for (int r = 0; r < R; ++r) {
       int64_t c = 0;
       if (next[s * R + r] >= 0)
@@ -308,7 +312,7 @@ void* oc_model_create(const oc_code* dec, double p, int64_t learn_len, int64_t b
       Mo->logp1[s * R + r] = log(v > 1e-300 ? v : 1e-300);
     }
   }
-  Mo->unseen = log(lam / ((double)S * lam));
+  Mo->unseen = log(lam / ((double)SL * lam));
   free(cnt);
   free(next);
   return Mo;

@@ -89,6 +89,40 @@ def test_native_sparse_model_equals_c_oracle(pkg):
         assert mod.info()["logp1_unseen"] == math.log(1.0 / om.S)
 
 
+# certified lower bound on the m = 6 (133,171) state count from the GPU BFS
+# (cvd_enumerate_device, profiles/r03b/bfs_m6.json)
+S_M6_LOWER = 3_192_590_107
+
+
+@pytest.mark.parametrize("S_lap", [S_M6_LOWER, 5_000_000_000_123])
+def test_laplace_states_model_equals_c_oracle(pkg, S_lap):
+    """The reference's estimator with a measured / bounded S in the Laplace denominator
+    (Pd_plotter.py:166-167; laplace_states): product host learning == C oracle given the
+    same S, row for row, bit for bit (numpy's pairwise row sum over S entries vs the
+    closed form R_i + S*laplace, equal for integral laplace)."""
+    cc = pkg.CONFIG_CODES["m6"]
+    mod = pkg.Model(pkg.Code(cc["gen1"], 6, 1, 2), 0.05, 50000, 200, 1.0, 12345, enum_cap=1000,
+                    laplace_states=S_lap)
+    om = C.Model(C.Code(cc["gen1"], 6, 1, 2), 0.05, 50000, 200, 1.0, 12345, enum_cap=1000, laplace_states=S_lap)
+    lp, keys = mod.rows()
+    olp, okeys = om.rows()
+    np.testing.assert_array_equal(keys, okeys)
+    assert np.array_equal(lp, olp)
+    inf = mod.info()
+    assert inf["S"] == S_lap and inf["n_rows"] == om.S == len(keys)
+    assert inf["logp1_unseen"] == math.log(1.0 / S_lap)
+
+
+def test_laplace_states_rejected_when_inconsistent(pkg):
+    cc = pkg.CONFIG_CODES["m6"]
+    with pytest.raises(pkg.CvdError, match="below the number of visited"):
+        pkg.Model(pkg.Code(cc["gen1"], 6, 1, 2), 0.05, 50000, 200, 1.0, 1, enum_cap=1000, laplace_states=10)
+    m2 = pkg.CONFIG_CODES["m2"]
+    with pytest.raises(pkg.CvdError, match="enumerable"):
+        pkg.Model(pkg.Code(m2["gen1"], 2, 1, 2), 0.05, None, 200, 1.0, 1, laplace_states=32)
+    assert pkg.Model(pkg.Code(m2["gen1"], 2, 1, 2), 0.05, None, 200, 1.0, 1, laplace_states=31).info()["S"] == 31
+
+
 def test_c_oracle_sparse_sums_vs_python(pkg):
     """C oracle m = 6 sums == Python recursion over the same rows (T_ref by
     comparing all 2^n successors)."""

@@ -69,3 +69,22 @@ def test_gpu_bfs_capacity_gives_lower_bound(pkg):
     out = pkg.enumerate_states_device(m6["gen1"], 6, 1, 2, device=0, cap=2_000_000)
     assert not out["complete"] and out["S"] > 2_000_000
     assert out["level_sizes"][0] == 1 and sum(out["level_sizes"]) == out["S"]
+
+
+def test_m6_detector_with_bfs_lower_bound_as_laplace_S(pkg):
+    """The reference's own estimator at the headline code with S = the GPU BFS's certified
+    lower bound in the Laplace denominator (laplace_states): the GPU detector's per-trial
+    fp64 sums and counts equal the C oracle's given the same S."""
+    from oracle import c_oracle as C
+    S_lap = 3_192_590_107
+    cc = pkg.CONFIG_CODES["m6"]
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    mod = det.model(0.02, 200_000, 200, 1.0, 12345, laplace_states=S_lap)
+    assert mod.info()["S"] == S_lap
+    N, T = 2000, 128
+    got = det.run_trials(mod, cc["gen1"], cc["gen2"], N, 0.02, 12345, 0, T, return_sums=True)
+    c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
+    om = C.Model(c1, 0.02, 200_000, 200, 1.0, 12345, enum_cap=1000, laplace_states=S_lap)
+    cnt, sums = om.run_trials(c1, c2, N, 0.02, 12345, 0, T, sums=True, nthreads=8)
+    assert np.array_equal(got["sums"], sums)
+    assert got["counts"].cpu().tolist() == [int(x) for x in cnt]
