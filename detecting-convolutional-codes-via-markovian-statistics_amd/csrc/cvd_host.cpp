@@ -519,6 +519,24 @@ void build_hash(cvd_model& Mo) {
   Mo.h_row.assign(interleave ? 0 : (size_t)cap * Mo.h_rsw, 0u);
   Mo.h_drow.assign((size_t)Mo.n_rows * Mo.h_rsw, 0u);
   Mo.max_probe = 0;
+  // Device row ids (drow index, successor fields, slot0): rows by descending visit count
+  // of the learning chain, which is the trial streams' own process (encoder G1, BSC(p)),
+  // so the rows table walks read most sit together in few cache lines instead of in
+  // first-visit order (CVD_ROW_ORDER=first keeps first-visit order).  Only the device
+  // numbering changes; lookups resolve to the same rows.
+  std::vector<int64_t> dev_of((size_t)Mo.n_rows);
+  for (int64_t i = 0; i < Mo.n_rows; ++i) dev_of[(size_t)i] = i;
+  {
+    const char* ro = std::getenv("CVD_ROW_ORDER");
+    const bool hot = !(ro && std::string(ro) == "first");
+    if (hot && (int64_t)Mo.visits.size() == Mo.n_rows) {
+      std::vector<int64_t> order((size_t)Mo.n_rows);
+      for (int64_t i = 0; i < Mo.n_rows; ++i) order[(size_t)i] = i;
+      std::stable_sort(order.begin(), order.end(),
+                       [&](int64_t x, int64_t y) { return Mo.visits[(size_t)x] > Mo.visits[(size_t)y]; });
+      for (int64_t k = 0; k < Mo.n_rows; ++k) dev_of[(size_t)order[(size_t)k]] = k;
+    }
+  }
   std::vector<int64_t> slot_of((size_t)Mo.n_rows);
   std::vector<uint32_t> kws((size_t)Mo.n_rows * nw), phs((size_t)Mo.n_rows), pls((size_t)Mo.n_rows);
   parallel_for(Mo.n_rows, [&](int64_t i, int) {
@@ -544,18 +562,18 @@ void build_hash(cvd_model& Mo) {
   parallel_for(Mo.n_rows, [&](int64_t i, int) {
     // entry r = 16 bytes {log P̂1[r] (f64), successor row (i32, -1: none), 0}: one
     // 12-byte device load per step
-    uint32_t* dw = Mo.h_drow.data() + (size_t)i * Mo.h_rsw;
+    uint32_t* dw = Mo.h_drow.data() + (size_t)dev_of[(size_t)i] * Mo.h_rsw;
     for (int r = 0; r < R; ++r) {
       std::memcpy(dw + 4 * r, Mo.logp1.data() + (size_t)i * R + r, sizeof(double));
       const int64_t j = Mo.row_next[(size_t)i * R + r];
-      dw[4 * r + 2] = (uint32_t)(j >= 0 ? (int32_t)j : -1);
+      dw[4 * r + 2] = (uint32_t)(j >= 0 ? (int32_t)dev_of[(size_t)j] : -1);
       dw[4 * r + 3] = 0u;
     }
     uint32_t* hw = interleave ? Mo.h_key.data() + (size_t)slot_of[(size_t)i] * ssw + nw
                               : Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw;
     std::memcpy(hw, dw, sizeof(uint32_t) * Mo.h_rsw);
   });
-  Mo.slot0 = 0;   // D_0 = 0 is row 0 in both model kinds
+  Mo.slot0 = (int32_t)dev_of[0];   // D_0 = 0 is row 0 in both model kinds
 }
 
 void build_bmk1(cvd_model& Mo, const Tabs& T) {
@@ -730,6 +748,9 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
     pt.mark("chain");
     Mo->n_rows = S;
     Mo->keys = std::move(states);
+    Mo->visits.assign((size_t)S, 0);
+    for (int64_t s2 = 0; s2 < S; ++s2)
+      for (int r = 0; r < R; ++r) Mo->visits[(size_t)s2] += cnt[(size_t)s2 * R + r];
     Mo->logp1.assign((size_t)S * R, 0.0);
     Mo->rec.assign((size_t)S * R, 0u);
     std::vector<int64_t> succ((size_t)R);
@@ -834,6 +855,9 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
     });
     pt.mark("successors + P1 rows");
     Mo->keys = std::move(keys);
+    Mo->visits.assign((size_t)rows, 0);
+    for (int64_t s2 = 0; s2 < rows; ++s2)
+      for (int r = 0; r < R; ++r) Mo->visits[(size_t)s2] += cnt[(size_t)s2 * R + r];
     std::vector<int64_t> none((size_t)R, -1), zc((size_t)R, 0);
     std::vector<double> lp((size_t)R);
     p1_row(S, prm->laplace, memo, none.data(), zc.data(), R, lp.data());
@@ -859,7 +883,7 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
 
 namespace {
 constexpr char kMagic[4] = {'C', 'V', 'D', 'M'};
-constexpr uint32_t kFileVersion = 1;
+constexpr uint32_t kFileVersion = 2;   // 2: + visits
 
 struct Writer {
   FILE* f;
@@ -911,7 +935,7 @@ extern "C" int cvd_model_save(const cvd_model* Mo, const char* path) {
   w.pod(Mo->kind); w.pod(Mo->S); w.pod(Mo->learn_len_eff); w.pod(Mo->laplace); w.pod(Mo->logp1_unseen);
   w.pod(Mo->n_rows);
   w.vec(Mo->ltref); w.vec(Mo->keys); w.vec(Mo->logp1); w.vec(Mo->rec); w.vec(Mo->rowsum);
-  w.vec(Mo->p1_nz); w.vec(Mo->row_next);
+  w.vec(Mo->p1_nz); w.vec(Mo->row_next); w.vec(Mo->visits);
   const bool ok = w.ok && std::fclose(f) == 0;
   if (!ok || std::rename(tmp.c_str(), path) != 0) {
     std::remove(tmp.c_str());
@@ -946,14 +970,14 @@ extern "C" int cvd_model_load(const char* path, cvd_model** out) {
   r.pod(Mo->kind); r.pod(Mo->S); r.pod(Mo->learn_len_eff); r.pod(Mo->laplace); r.pod(Mo->logp1_unseen);
   r.pod(Mo->n_rows);
   r.vec(Mo->ltref); r.vec(Mo->keys); r.vec(Mo->logp1); r.vec(Mo->rec); r.vec(Mo->rowsum);
-  r.vec(Mo->p1_nz); r.vec(Mo->row_next);
+  r.vec(Mo->p1_nz); r.vec(Mo->row_next); r.vec(Mo->visits);
   const CodeDesc& d = Mo->dec;
   const bool shape_ok = d.k >= 1 && d.k <= kMaxK && d.n >= 1 && d.n <= kMaxN && d.m >= 1 && d.m <= kMaxM;
   const size_t M = shape_ok ? (size_t)1 << d.m : 0, R = shape_ok ? (size_t)1 << d.n : 0;
   bool valid = r.ok && shape_ok && (Mo->kind == 0 || Mo->kind == 1) && Mo->n_rows >= 1 &&
                Mo->n_rows < ((int64_t)1 << 31) && Mo->keys.size() == (size_t)Mo->n_rows * M &&
                Mo->logp1.size() == (size_t)Mo->n_rows * R && Mo->row_next.size() == (size_t)Mo->n_rows * R &&
-               Mo->ltref.size() == R + 1;
+               Mo->ltref.size() == R + 1 && Mo->visits.size() == (size_t)Mo->n_rows;
   // dense models: S rows, one 32-bit record and one row sum per (row, word) / row,
   // every record's successor a row; sparse: S = rows.  Successors must be rows or
   // -1, and every metric byte a nibble: the device tables are built from these

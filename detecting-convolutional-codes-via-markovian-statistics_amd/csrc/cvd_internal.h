@@ -27,6 +27,8 @@ struct cvd_model {
   struct NZ { int64_t row, col; double val; };
   std::vector<double> rowsum;     // dense only: numpy row sums of counts + λ
   std::vector<NZ> p1_nz;          // dense only: entries with counts (value = C + λ)
+  std::vector<int64_t> visits;    // [n_rows] learning-chain visits counted (t in [burn, L)): the
+                                  // device numbers rows by it (hot rows share cache lines)
 
   // explicit-path hash over nibble-packed keys
   int64_t hcap = 0;               // power of two, 0 = none

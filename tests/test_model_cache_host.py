@@ -108,7 +108,9 @@ def test_load_rejects_corrupt_successor_and_foreign_code(pkg, golden, tmp_path):
     path = tmp_path / "m.bin"
     a.save(path)
     raw = bytearray(path.read_bytes())
-    raw[-8:] = np.int64(a.info()["n_rows"] + 5).tobytes()   # last successor entry out of range
+    n = a.info()["n_rows"]
+    o = len(raw) - 8 * n - 8 - 8       # the last successor entry (the visits vector follows it)
+    raw[o:o + 8] = np.int64(n + 5).tobytes()   # out of range
     bad = tmp_path / "bad.bin"
     bad.write_bytes(bytes(raw))
     with pytest.raises(pkg.CvdError, match="corrupt"):
