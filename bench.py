@@ -44,6 +44,7 @@ sys.path.insert(0, ROOT)
 METRIC = "MC trials/sec at N=1e5, rate-1/2 m=6 pair, 1/2/4/8 GPUs; Pd match vs CPU"
 P_GRID = [0.01, 0.02, 0.05, 0.10, 0.15, 0.20]
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+LDS_PEAK_GBS = 256 * 256 * 2.4   # 256 CUs x 256 B/clk (ds_read_b64, MI355X_MICROARCH.md LDS) x 2.4 GHz
 # VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
 SHADER_GHZ = 2.4
@@ -96,6 +97,10 @@ def parse():
     ap.add_argument("--overlap", type=int, default=-1,
                     help="generate the next batch on a second stream while the detector runs "
                          "(-1: auto = on for the table automaton, where it measured faster)")
+    ap.add_argument("--fused", type=int, default=-1,
+                    help="dense (table-automaton) configs: generator and detector in ONE kernel per step "
+                         "(cvd_mc_fused: each lane generates its own words and feeds the LDS-resident "
+                         "automaton, no streams in HBM); -1: auto = on for dense models")
     ap.add_argument("--cpu-baseline", type=int, default=1,
                     help="time the C oracle port on this host (rank 0, one GPU), check Pd against it at "
                          "the config's informative point, and run the C0 demo preset on both sides")
@@ -192,18 +197,24 @@ def main():
     # double-buffered pipeline: the generator fills buffer (s+1)%2 on its own
     # stream while the detector reads buffer s%2 (both kernels of every timed
     # step run inside the timed region)
+    if a.fused < 0:
+        a.fused = int(not parity and not info["kind"])
+    if a.fused:
+        a.overlap = 0
     if a.overlap < 0:
         a.overlap = int(not info["kind"])
     buf_bytes = det.words_per_seq(N) * 4 * 2 * B
     if a.overlap and 2 * buf_bytes > (120 << 30):
         a.overlap = 0                          # two batches would not leave HBM headroom
     nbuf = 2 if a.overlap else 1
-    bufs = [det.stream_buffer(N, 2 * B) for _ in range(nbuf)]
+    bufs = [] if a.fused else [det.stream_buffer(N, 2 * B) for _ in range(nbuf)]
     counts = torch.zeros((len(p_grid), 2), dtype=torch.int64, device=det.device)
     dstream = torch.cuda.current_stream()
     gstream = torch.cuda.Stream(device=det.device) if a.overlap else dstream
 
     def gen(s, ev=None):
+        if a.fused:
+            return   # the fused kernel generates its own words (detect below)
         p = p_grid[s % len(p_grid)]
         tb = (s * world + rank) * B            # global trial ids of this rank's batch
         tag = pkg.grid_tag(N, p)
@@ -224,6 +235,10 @@ def main():
         if parity:
             pkg.parity_detect(bufs[s % nbuf], n, N, 2 * B, B, tpl, a.gamma, counts=counts[s % len(p_grid)],
                               stream=dstream)
+        elif a.fused:
+            tb = (s * world + rank) * B            # global trial ids of this rank's batch
+            det.run_trials(models[p], cc["gen1"], cc["gen2"], N, p, a.seed, tb, tb + B,
+                           counts=counts[s % len(p_grid)], stream=dstream, early_decision=early[0], fused=True)
         else:
             det.detect(models[p], bufs[s % nbuf], N, 2 * B, B, counts=counts[s % len(p_grid)], stream=dstream,
                        early_decision=early[0])
@@ -279,7 +294,7 @@ def main():
 
     if dist:
         elapsed = max_over_ranks(elapsed)
-    gen_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    gen_ms = 0.0 if a.fused else float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     det_each = [e[2].elapsed_time(e[3]) for e in events]
     det_ms = float(np.mean(det_each))
 
@@ -324,14 +339,21 @@ def main():
     # received streams read once, 2 * ceil(N * n / 8) bytes per trial
     alg_bytes = B * 2 * ((N * n + 7) // 8)
     achieved = alg_bytes / (det_ms * 1e-3) / 1e9
+    if a.fused:
+        # no stream in HBM: the fused kernel is bound by its LDS gathers (per sequence-step
+        # one 16-bit record and two f64 entries, 18 B) and the generator's VALU; LDS peak
+        # 256 B/clk/CU (MI355X_MICROARCH.md, LDS: ds_read_b64) x 256 CUs x 2.4 GHz
+        alg_bytes = B * 2 * N * 18
+        achieved = alg_bytes / (det_ms * 1e-3) / 1e9
     traffic, traffic_src, pmc = None, None, None
     if a.pmc_traffic is None:
         a.pmc_traffic = os.path.join(ROOT, "profiles", f"pmc_{a.detector}_{a.config}.json")
     if a.pmc_traffic and os.path.exists(a.pmc_traffic):
         with open(a.pmc_traffic) as f:
             pmc = json.load(f)
-        if (pmc.get("config"), pmc.get("batch"), pmc.get("N"), pmc.get("detector", "markov")) != \
-                (a.config, B, N, a.detector) or sorted(pmc.get("per_p", {})) != sorted(str(p) for p in p_grid):
+        if (pmc.get("config"), pmc.get("batch"), pmc.get("N"), pmc.get("detector", "markov"),
+                bool(pmc.get("fused", False))) != (a.config, B, N, a.detector, bool(a.fused)) or \
+                sorted(pmc.get("per_p", {})) != sorted(str(p) for p in p_grid):
             pmc = None   # counters of another workload (or of a single-p diagnostic run)
     valu = None
     traffic_by_p, gen_pmc = None, None
@@ -388,9 +410,13 @@ def main():
                    "model": info["kind"] and "sparse(learned)" or "dense",
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
-        "roofline": {"bound": "valu" if valu else "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "roofline": {"bound": "lds" if a.fused else "valu" if valu else "hbm", "achieved": achieved,
+                     "peak": LDS_PEAK_GBS if a.fused else HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / (LDS_PEAK_GBS if a.fused else HBM_PEAK_GBS),
+                     "traffic": traffic,
                      "kernel": ("parity_kernel (parity-template baseline, cvd_parity.hip)" if parity
+                                else "mc_table16_kernel (generator + LDS table automaton fused, cvd_mc_fused; "
+                                     "achieved = LDS gather bytes)" if a.fused
                                 else pkg.KERNEL_NAMES[info["explicit_kernel"]] if info["kind"]
                                 else "detect_table_kernel (enumerated state automaton)"),
                      "traffic_source": traffic_src,
@@ -399,7 +425,7 @@ def main():
                      "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms,
                      "valu": valu},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
-                       "overlap": bool(a.overlap), "model_setup_s": t_setup,
+                       "overlap": bool(a.overlap), "fused": bool(a.fused), "model_setup_s": t_setup,
                        "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
                        "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
                        "detector_ms_steps": det_each,

@@ -98,6 +98,10 @@ EXPORTS = {
                                   ctypes.c_double, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_int32, ctypes.c_void_p]),
+    "cvd_mc_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_code),
+                                    ctypes.c_double, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
+                                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                    ctypes.c_void_p]),
     "cvd_parity_detect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
                                          ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

@@ -88,6 +88,12 @@ int launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag,
                     uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream);
 int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                         int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream, bool early = false);
+// the whole trial loop in one kernel (generator + LDS table automaton, no streams in
+// HBM): trials [trial_begin, trial_begin + T) of one grid point; CVD_E_UNSUPPORTED if
+// the model / codes do not fit it
+int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
+                    uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,
+                    int64_t* d_counts, void* stream, bool early);
 int launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                            int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
                            void* stream, int variant, bool early = false);

@@ -218,20 +218,24 @@ __device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMI
 //  * Planes 1-8 (Philox blocks 0 and 1) of all four words run unconditionally.  A code
 //    bit is then still undecided with probability 2^-8, so ~12% of the wave's 256
 //    (lane, word) pairs hold one (~30).
-//  * Those pairs are compacted into consecutive lanes through LDS: slot i computes the
-//    next two blocks (8 planes) of the i-th pair and the result goes back to the owner.
-//    After 16 planes ~0.1 undecided bits are left per wave and chunk; a further pass runs
-//    only while the ballot finds one.
+//  * Those pairs are compacted into consecutive lanes through LDS (su, sm: 64 words
+//    each per wave): slot i computes the next two blocks (8 planes) of the i-th pair
+//    and the result goes back to the owner.  After 16 planes ~0.1 undecided bits are
+//    left per wave and chunk; a further pass runs only while the ballot finds one.
+//  * seq(l): the (counter word 1, counter word 2) = (seq_lo, ctr_hi(seq, noise)) of
+//    lane l's sequence, for the slot lanes (LDS copies in gen_fast_kernel, computed
+//    from the lane index in the fused kernel).
 // One word at a time (3 blocks for every lane, then single blocks while any lane is
 // undecided) costs ~3.4 blocks per word; this ~2.5.
-__device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, NoiseLds& sh, uint32_t nhi, uint32_t w4,
+template <typename Seq>
+__device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
                                                  const bool (&live)[4], uint32_t valid, uint32_t (&F)[4]) {
   const uint32_t t = a.thr_lo, lane = lane_id();
   const uint32_t nslots = a.slots - 1u < 64u ? a.slots : 64u;   // 1..64: every round makes progress
   uint32_t U[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) { U[g] = live[g] ? valid : 0u; F[g] = 0u; }
-  const uint32_t slo = sh.slo[lane];
+  const uint2 own = seq(lane);
 #pragma unroll
   for (int g = 0; g < 4; ++g) {   // blocks 0 and 1 of word g
     const uint32_t k0 = a.k0, k1 = a.k1;
@@ -239,7 +243,7 @@ __device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, NoiseLds& sh,
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       xv[b][0] = (w4 + g) * kNoiseBlocksPerWord + (uint32_t)b;
-      xv[b][1] = slo; xv[b][2] = nhi; xv[b][3] = a.tag;
+      xv[b][1] = own.x; xv[b][2] = own.y; xv[b][3] = a.tag;
     }
     philox_blocks<2>(xv, k0, k1);
     noise_planes4(t >> 28, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U[g], F[g]);
@@ -259,68 +263,76 @@ __device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, NoiseLds& sh,
     for (uint32_t s0 = 0; s0 < tot; s0 += nslots) {   // rounds of 64 slots (nearly always one)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        if (U[g] != 0u && slot[g] - s0 < nslots) { sh.u[slot[g] - s0] = U[g]; sh.m[slot[g] - s0] = lane | (uint32_t)g << 6; }
+        if (U[g] != 0u && slot[g] - s0 < nslots) { su[slot[g] - s0] = U[g]; sm[slot[g] - s0] = lane | (uint32_t)g << 6; }
       wave_lds_sync();
       const bool busy = lane < nslots && s0 + lane < tot;
       if (busy) {
-        uint32_t Un = sh.u[lane], Fn = 0u;
-        const uint32_t mm = sh.m[lane], src = mm & 63u, w = w4 + (mm >> 6);
+        uint32_t Un = su[lane], Fn = 0u;
+        const uint32_t mm = sm[lane], src = mm & 63u, w = w4 + (mm >> 6);
         const uint32_t k0 = a.k0, k1 = a.k1;
+        const uint2 sq = seq(src);
         uint32_t xv[2][4];
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           xv[b][0] = w * kNoiseBlocksPerWord + j + (uint32_t)b;
-          xv[b][1] = sh.slo[src]; xv[b][2] = sh.nhi[src]; xv[b][3] = a.tag;
+          xv[b][1] = sq.x; xv[b][2] = sq.y; xv[b][3] = a.tag;
         }
         philox_blocks<2>(xv, k0, k1);
         noise_planes4(t >> (28u - 4u * j), xv[0][0], xv[0][1], xv[0][2], xv[0][3], Un, Fn);
         noise_planes4(t >> (24u - 4u * j), xv[1][0], xv[1][1], xv[1][2], xv[1][3], Un, Fn);
-        sh.u[lane] = Un; sh.m[lane] = Fn;
+        su[lane] = Un; sm[lane] = Fn;
       }
       wave_lds_sync();
 #pragma unroll
       for (int g = 0; g < 4; ++g)   // owners (U still holds the value they sent)
-        if (U[g] != 0u && slot[g] - s0 < nslots) { U[g] = sh.u[slot[g] - s0]; F[g] |= sh.m[slot[g] - s0]; }
+        if (U[g] != 0u && slot[g] - s0 < nslots) { U[g] = su[slot[g] - s0]; F[g] |= sm[slot[g] - s0]; }
       wave_lds_sync();
     }
   }
 }
 
+// Encoder of one sequence, one received word at a time (bit-parallel, see above):
+// the input stream's Philox block cache and the window history carried from word
+// to word.  encode(w, nm) returns word w with the flip mask nm applied.
 template <int k, int n>
-__global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
-  constexpr int SPW = 32 / n, NBITS = SPW * n;
-  constexpr uint32_t kValid = NBITS == 32 ? ~0u : (1u << (NBITS % 32)) - 1u;
-  static_assert(k >= 1 && k <= 2 && SPW * k <= 32, "gen_fast_kernel: shape");
-  const int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  // lanes past the end stay in the wave (U = 0, no stores): the noise exchange
-  // uses every lane of the wave as a slot
-  const bool lane_ok = li < a.count;
-  const int64_t q = a.q0 + li;
-  const uint64_t sid = (uint64_t)(a.seq_base + li * a.seq_stride);
-  const uint32_t slo = (uint32_t)sid, nhi = ctr_hi(sid, kKindNoise), ihi = ctr_hi(sid, kKindInput);
-  __shared__ NoiseLds noise_lds[kBlock / 64];
-  NoiseLds& nl = noise_lds[threadIdx.x / 64];
-  nl.slo[lane_id()] = slo;
-  nl.nhi[lane_id()] = nhi;
-  wave_lds_sync();
-  const int hs = a.hs;
-  const int64_t nwords = (a.N + SPW - 1) / SPW;
-  const int64_t nw4 = (nwords + 3) & ~(int64_t)3;
-  int64_t iblk = -1;
-  U4 iv{0u, 0u, 0u, 0u};
-  auto input_word = [&](int64_t W) -> uint32_t {   // 32-bit word W of the input stream
+struct ChunkEncoder {
+  static constexpr int SPW = 32 / n, NBITS = SPW * n;
+  static constexpr uint32_t kValid = NBITS == 32 ? ~0u : (1u << (NBITS % 32)) - 1u;
+  // k = 1 (spread-first): the input bits are Morton-spread once per word (bit i ->
+  // bit n*i), and the window W = U << hs | (history) is kept in that spread form as
+  // 64 bits (lo, hi): every tap W >> sh is then one v_alignbit by n*sh of (hi, lo),
+  // already at the output's bit positions, so the n outputs need no spread of their
+  // own (m2 generator 12.1 -> 11.6 ms, m = 6 8.6 -> 8.3 ms alone).  sprev: the
+  // previous word's spread inputs (the history is its top hs steps).
+  // k = 2 keeps plain windows and one spread per output: spread-first made the
+  // rate-2/3 generator faster alone (16.1 -> 15.8 ms) but the overlapped C3 step
+  // 1.7% slower (profiles/r02z_gen/ab_enc_*.json).
+  static constexpr bool kSpreadFirst = k == 1;
+  const GenArgs* a;
+  uint32_t slo, ihi;
+  int64_t iblk;
+  U4 iv;
+  uint32_t sprev[k], hist[k];
+  __device__ void init(const GenArgs* a_, uint64_t sid) {
+    a = a_;
+    slo = (uint32_t)sid; ihi = ctr_hi(sid, kKindInput);
+    iblk = -1; iv = U4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int r = 0; r < k; ++r) sprev[r] = hist[r] = 0u;   // encoder starts in state 0
+  }
+  __device__ uint32_t input_word(int64_t W) {   // 32-bit word W of the input stream
     if ((W >> 2) != iblk) {
       iblk = W >> 2;
-      uint32_t k0 = a.k0, k1 = a.k1;
+      uint32_t k0 = a->k0, k1 = a->k1;
       asm volatile("" : "+s"(k0), "+s"(k1));
-      iv = philox((uint32_t)iblk, slo, ihi, a.tag, k0, k1);
+      iv = philox((uint32_t)iblk, slo, ihi, a->tag, k0, k1);
     }
     return u4_get(iv, (uint32_t)(W & 3));
-  };
+  }
   // input bits [w*SPW*k, (w+1)*SPW*k) of the flat input stream, split by phase
-  auto word_inputs = [&](int64_t w, uint32_t (&U)[k]) {
+  __device__ void word_inputs(int64_t w, uint32_t (&U)[k]) {
     uint32_t Fw = 0u;
-    if (a.random_input) {
+    if (a->random_input) {
       const int64_t b0 = w * SPW * k;
       const uint32_t off = (uint32_t)(b0 & 31);
       const uint32_t lo = input_word(b0 >> 5);
@@ -332,102 +344,118 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
 #pragma unroll
     for (int r = 0; r < k; ++r)
       if constexpr (SPW < 32) U[r] &= (1u << SPW) - 1u;
-  };
+  }
+  // history of a segment starting at word w0 > 0: the hs input steps before it
+  __device__ void seek(int64_t w0) {
+    uint32_t Up[k];
+    word_inputs(w0 - 1, Up);
+#pragma unroll
+    for (int r = 0; r < k; ++r) {
+      if constexpr (kSpreadFirst) sprev[r] = spread_n<n>(Up[r]);
+      else hist[r] = (Up[r] >> (SPW - a->hs)) & ((1u << a->hs) - 1u);
+    }
+  }
+  __device__ uint32_t encode(int64_t w, uint32_t nm) {
+    const int hs = a->hs;
+    const uint32_t nhs = (uint32_t)(n * hs), nrest = (uint32_t)(n * (SPW - hs));   // 0 < nhs < 32, nrest < 32
+    uint32_t U[k];
+    word_inputs(w, U);
+    uint32_t lo[k], hi[k];   // spread-first windows, or the plain windows in lo
+#pragma unroll
+    for (int r = 0; r < k; ++r) {
+      if constexpr (kSpreadFirst) {
+        const uint32_t su = spread_n<n>(U[r]);
+        lo[r] = (su << nhs) | (sprev[r] >> nrest);
+        hi[r] = su >> (32u - nhs);
+        sprev[r] = su;
+      } else {
+        lo[r] = (U[r] << hs) | hist[r];
+        hi[r] = 0u;
+        hist[r] = (lo[r] >> SPW) & ((1u << hs) - 1u);
+      }
+    }
+    uint32_t word = 0u;
+#pragma unroll
+    for (int j = 0; j < n; ++j) {
+      uint32_t o = 0u;
+#pragma unroll
+      for (int r = 0; r < k; ++r) {
+        // the set taps only, as a scalar loop over the uniform mask (s_ff1):
+        // two VALU per tap.  The mask is re-read per word -- hoisted out of
+        // the chunk loop, per-shift conditions filled the SGPRs (spills) and
+        // unrolled they became selects for every possible shift
+        uint32_t tm = a->taps[j][r];
+        asm volatile("" : "+s"(tm));
+#pragma nounroll
+        while (tm) {
+          const uint32_t sh = (uint32_t)__builtin_ctz(tm);
+          tm &= tm - 1u;
+          if constexpr (kSpreadFirst) o ^= __builtin_amdgcn_alignbit(hi[r], lo[r], (uint32_t)n * sh);
+          else o ^= lo[r] >> sh;
+        }
+      }
+      if constexpr (kSpreadFirst) {
+        word |= o << j;
+      } else {
+        if constexpr (SPW < 32) o &= (1u << SPW) - 1u;
+        word |= spread_n<n>(o) << j;
+      }
+    }
+    if constexpr (kSpreadFirst && NBITS < 32) word &= kValid;   // n = 3: step SPW's bits at 30, 31
+    word ^= nm;
+    const int64_t ns = a->N - w * SPW;           // steps in this word (last word: < SPW)
+    if (ns < SPW) word &= (1u << (n * ns)) - 1u;
+    return word;
+  }
+  // flip masks and words w4 .. w4 + 3 (wave-collective: every lane of the wave calls
+  // it for the same w4; live[g] = word w4 + g exists for this lane)
+  template <typename Seq>
+  __device__ void chunk(uint32_t* su, uint32_t* sm, Seq seq, int64_t w4, const bool (&live)[4], int64_t nwords,
+                        uint32_t (&out4)[4]) {
+    uint32_t nm4[4] = {0u, 0u, 0u, 0u};
+    if (a->thr_all) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) nm4[g] = kValid;
+    } else if (a->thr_lo) {
+      noise_chunk_wave(*a, su, sm, seq, (uint32_t)w4, live, kValid, nm4);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) out4[g] = w4 + g < nwords ? encode(w4 + g, nm4[g]) : 0u;
+  }
+};
+
+template <int k, int n>
+__global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
+  constexpr int SPW = 32 / n;
+  static_assert(k >= 1 && k <= 2 && SPW * k <= 32, "gen_fast_kernel: shape");
+  const int64_t li = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  // lanes past the end stay in the wave (U = 0, no stores): the noise exchange
+  // uses every lane of the wave as a slot
+  const bool lane_ok = li < a.count;
+  const int64_t q = a.q0 + li;
+  const uint64_t sid = (uint64_t)(a.seq_base + li * a.seq_stride);
+  __shared__ NoiseLds noise_lds[kBlock / 64];
+  NoiseLds& nl = noise_lds[threadIdx.x / 64];
+  nl.slo[lane_id()] = (uint32_t)sid;
+  nl.nhi[lane_id()] = ctr_hi(sid, kKindNoise);
+  wave_lds_sync();
+  auto seq = [&](uint32_t l) { return make_uint2(nl.slo[l], nl.nhi[l]); };
+  const int64_t nwords = (a.N + SPW - 1) / SPW;
+  const int64_t nw4 = (nwords + 3) & ~(int64_t)3;
+  ChunkEncoder<k, n> enc;
+  enc.init(&a, sid);
   // segment blockIdx.y of the sequence's 16-byte chunks: every word depends only
   // on its own inputs and the hs input steps before it, so segments are
   // independent (more waves in flight than one lane per sequence gives)
   const int64_t nchunks = nw4 >> 2, seg = gridDim.y;
   const int64_t c0 = nchunks * blockIdx.y / seg, c1 = nchunks * (blockIdx.y + 1) / seg;
-  // k = 1 (spread-first): the input bits are Morton-spread once per word (bit i ->
-  // bit n*i), and the window W = U << hs | (history) is kept in that spread form as
-  // 64 bits (lo, hi): every tap W >> sh is then one v_alignbit by n*sh of (hi, lo),
-  // already at the output's bit positions, so the n outputs need no spread of their
-  // own (m2 generator 12.1 -> 11.6 ms, m = 6 8.6 -> 8.3 ms alone).  sprev: the
-  // previous word's spread inputs (the history is its top hs steps).
-  // k = 2 keeps plain windows and one spread per output: spread-first made the
-  // rate-2/3 generator faster alone (16.1 -> 15.8 ms) but the overlapped C3 step
-  // 1.7% slower (profiles/r02z_gen/ab_enc_*.json).
-  constexpr bool kSpreadFirst = k == 1;
-  uint32_t sprev[k], hist[k];
-#pragma unroll
-  for (int r = 0; r < k; ++r) sprev[r] = hist[r] = 0u;   // encoder starts in state 0
-  if (c0 > 0 && 4 * c0 <= nwords) {
-    uint32_t Up[k];
-    word_inputs(4 * c0 - 1, Up);
-#pragma unroll
-    for (int r = 0; r < k; ++r) {
-      if constexpr (kSpreadFirst) sprev[r] = spread_n<n>(Up[r]);
-      else hist[r] = (Up[r] >> (SPW - hs)) & ((1u << hs) - 1u);
-    }
-  }
-  const uint32_t nhs = (uint32_t)(n * hs), nrest = (uint32_t)(n * (SPW - hs));   // 0 < nhs < 32, nrest < 32
+  if (c0 > 0 && 4 * c0 <= nwords) enc.seek(4 * c0);
   for (int64_t w4 = 4 * c0; w4 < 4 * c1; w4 += 4) {
-    uint32_t nm4[4] = {0u, 0u, 0u, 0u};
     bool live[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) live[g] = lane_ok && w4 + g < nwords;
-    if (a.thr_all) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) nm4[g] = kValid;
-    } else if (a.thr_lo) {
-      noise_chunk_wave(a, nl, nhi, (uint32_t)w4, live, kValid, nm4);
-    }
     uint32_t out4[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int64_t w = w4 + g;
-      uint32_t word = 0u;
-      if (w < nwords) {
-        const uint32_t nm = nm4[g];
-        uint32_t U[k];
-        word_inputs(w, U);
-        uint32_t lo[k], hi[k];   // spread-first windows, or the plain windows in lo
-#pragma unroll
-        for (int r = 0; r < k; ++r) {
-          if constexpr (kSpreadFirst) {
-            const uint32_t su = spread_n<n>(U[r]);
-            lo[r] = (su << nhs) | (sprev[r] >> nrest);
-            hi[r] = su >> (32u - nhs);
-            sprev[r] = su;
-          } else {
-            lo[r] = (U[r] << hs) | hist[r];
-            hi[r] = 0u;
-            hist[r] = (lo[r] >> SPW) & ((1u << hs) - 1u);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < n; ++j) {
-          uint32_t o = 0u;
-#pragma unroll
-          for (int r = 0; r < k; ++r) {
-            // the set taps only, as a scalar loop over the uniform mask (s_ff1):
-            // two VALU per tap.  The mask is re-read per word -- hoisted out of
-            // the chunk loop, per-shift conditions filled the SGPRs (spills) and
-            // unrolled they became selects for every possible shift
-            uint32_t tm = a.taps[j][r];
-            asm volatile("" : "+s"(tm));
-#pragma nounroll
-            while (tm) {
-              const uint32_t sh = (uint32_t)__builtin_ctz(tm);
-              tm &= tm - 1u;
-              if constexpr (kSpreadFirst) o ^= __builtin_amdgcn_alignbit(hi[r], lo[r], (uint32_t)n * sh);
-              else o ^= lo[r] >> sh;
-            }
-          }
-          if constexpr (kSpreadFirst) {
-            word |= o << j;
-          } else {
-            if constexpr (SPW < 32) o &= (1u << SPW) - 1u;
-            word |= spread_n<n>(o) << j;
-          }
-        }
-        if constexpr (kSpreadFirst && NBITS < 32) word &= kValid;   // n = 3: step SPW's bits at 30, 31
-        word ^= nm;
-        const int64_t ns = a.N - w * SPW;           // steps in this word (last word: < SPW)
-        if (ns < SPW) word &= (1u << (n * ns)) - 1u;
-      }
-      out4[g] = word;
-    }
+    enc.chunk(nl.u, nl.m, seq, w4, live, nwords, out4);
     if (lane_ok)
       *reinterpret_cast<uint4*>(a.r + chunk_index(w4 >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
   }
@@ -579,6 +607,100 @@ __global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
     early_final(dec, lp, lr);
   }
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
+}
+
+// ─────────────── fused trial loop: generator + table automaton ───────────────
+//
+// The whole trial (Pd_plotter.py:210-223) in one kernel for the LDS-resident table
+// path: every lane generates its own sequence's received words four at a time
+// (ChunkEncoder: the same encoder and bit-sliced noise as gen_fast_kernel, so the
+// same streams bit for bit) and feeds them straight into the table steps of
+// detect_table16_kernel, with no stream in HBM.  The table path is LDS-bound and
+// the generator VALU-bound, so inside one wave's instruction stream the two
+// overlap: the two-kernel pipeline measured 39.6 ms (generator) against 29.7 ms
+// (detector) per overlapped m2 step, each ~24 ms alone.  Lanes [0, Tp) are H1
+// (encoder G1, sequence 2 (trial_begin + t)), [Tp, 2 Tp) H2 (G2, 2 (...) + 1); Tp is
+// the trial count rounded up to whole waves, so every wave is one hypothesis.
+struct FusedArgs {
+  TabArgs t;               // model tables, N, sums ([T][4]: lp1, lr1, lp2, lr2), counts, early
+  GenArgs g[2];            // H1 and H2 encoders, noise threshold, stream key
+  int64_t trial_begin, T, Tp;
+};
+
+template <int k, int n, int BS>
+__global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
+  constexpr int R = 1 << n, SPW = 32 / n;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const TabArgs& ta = a.t;
+  const int SR = (int)ta.S * R;
+  double* s_lp = reinterpret_cast<double*>(smem);
+  double* s_lt = s_lp + SR;
+  uint16_t* s_rec = reinterpret_cast<uint16_t*>(s_lt + R + 1);
+  // the noise exchange's slot records, 2 x 64 words per wave, after the model
+  uint32_t* s_x = reinterpret_cast<uint32_t*>(smem + (((size_t)SR * 10 + (R + 1) * 8 + 15) & ~(size_t)15));
+  for (int i = threadIdx.x; i < SR; i += BS) {
+    s_lp[i] = ta.logp1[i];
+    s_rec[i] = (uint16_t)ta.rec[i];    // next < 4096: next << 4 | c fits 16 bits (host-checked)
+  }
+  for (int i = threadIdx.x; i <= R; i += BS) s_lt[i] = ta.ltref[i];
+  __syncthreads();
+  uint32_t* su = s_x + (threadIdx.x / 64) * 128;
+  uint32_t* sm = su + 64;
+  // wave-uniform hypothesis (SGPR): the wave's first lane index
+  const int64_t wli = (int64_t)blockIdx.x * BS + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const int h = wli >= a.Tp ? 1 : 0;
+  const GenArgs& g = a.g[h];
+  const int64_t t0 = wli - (h ? a.Tp : 0);        // trial offset of lane 0
+  const uint32_t lane = lane_id();
+  const int64_t t = t0 + lane;
+  const bool valid = wli < 2 * a.Tp && t < a.T;
+  const uint64_t sid0 = 2 * (uint64_t)(a.trial_begin + t0) + (uint64_t)h;
+  auto seq = [&](uint32_t l) {
+    const uint64_t sd = sid0 + 2 * (uint64_t)l;
+    return make_uint2((uint32_t)sd, ctr_hi(sd, kKindNoise));
+  };
+  ChunkEncoder<k, n> enc;
+  enc.init(&g, sid0 + 2 * (uint64_t)lane);
+  const int64_t N = ta.N, nwords = (N + SPW - 1) / SPW, nchunks = (nwords + 3) / 4;
+  const int64_t full = N / (4 * SPW);             // chunks whose 4 words are all full
+  double lp = 0.0, lr = 0.0;
+  uint32_t st = 0;                                // index of D_0 = 0 (first BFS state)
+  int dec = 0;                                    // early decision (0 = open)
+  for (int64_t c = 0; c < nchunks; ++c) {
+    if (ta.early && c > 0 && (c & 1) == 0 && c <= full) {   // every 2 chunks (8 words)
+      if (!dec) dec = early_decide(lp, lr, N - c * 4 * SPW, ta.lt_min, ta.lp_min);
+      if (__ballot(dec == 0) == 0) break;         // the whole wave: the exchange stays collective
+    }
+    bool live[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) live[e] = valid && 4 * c + e < nwords;
+    uint32_t wv[4];
+    enc.chunk(su, sm, seq, 4 * c, live, nwords, wv);
+    if (c < full) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        uint32_t word = wv[e];
+#pragma unroll
+        for (int i = 0; i < SPW; ++i) {
+          const uint32_t idx = st * (uint32_t)R + (word & (uint32_t)(R - 1));
+          word >>= n;
+          const uint32_t rv = s_rec[idx];
+          lp += s_lp[idx];                        // log P̂1[i, j]   (Pd_plotter.py:213)
+          lr += s_lt[rv & 15u];                   // log T_ref[i, j] (Pd_plotter.py:214)
+          st = rv >> 4;
+        }
+      }
+    } else {
+      for (int e = 0; e < 4; ++e) {
+        const int64_t s0 = (4 * c + e) * SPW;
+        if (s0 >= N) break;
+        table16_word<n>(wv[e], (int)min((int64_t)SPW, N - s0), st, lp, lr, s_rec, s_lp, s_lt);
+      }
+    }
+  }
+  if (valid && ta.sums) { ta.sums[4 * t + 2 * h] = lp; ta.sums[4 * t + 2 * h + 1] = lr; }
+  early_final(dec, lp, lr);
+  count_decisions(valid, h == 0, lp, lr, ta.counts);
 }
 
 // pk16 minimum over L registers as a log-depth tree (independent ops issue back to back)
@@ -981,16 +1103,15 @@ int cvd::check_device(const cvd_model& M) {
   return CVD_OK;
 }
 
-int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, uint64_t thr,
-                         int64_t N, int random_input, int64_t seq_base, int64_t seq_stride,
-                         uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream) {
-  if (count <= 0 || N <= 0) return CVD_OK;
+namespace {
+// GenArgs of an encoder (the bit-parallel generator's window taps included)
+GenArgs gen_args(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, uint64_t thr, int64_t N,
+                 int random_input) {
   GenArgs a;
   a.enc = enc; a.k0 = k0; a.k1 = k1; a.tag = tag;
   a.thr_all = thr >= (1ull << 32); a.thr_lo = (uint32_t)std::min<uint64_t>(thr, 0xFFFFFFFFull);
-  a.random_input = random_input; a.N = N; a.seq_base = seq_base; a.seq_stride = seq_stride;
-  a.pitch = pitch; a.q0 = q0; a.count = count; a.r = d_r;
-  const unsigned grid = (unsigned)((count + kBlock - 1) / kBlock);
+  a.random_input = random_input; a.N = N;
+  a.seq_base = 0; a.seq_stride = 1; a.pitch = 0; a.q0 = 0; a.count = 0; a.r = nullptr;
   // bit-parallel generator: window taps per (output j, input phase r)
   a.hs = (enc.m + enc.k - 1) / enc.k;
   for (int j = 0; j < kMaxN; ++j) a.taps[j][0] = a.taps[j][1] = 0u;
@@ -1006,7 +1127,25 @@ int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t
     const char* e = std::getenv("CVD_GEN_SLOTS");
     a.slots = e ? (uint32_t)std::min(64, std::max(1, std::atoi(e))) : 64u;
   }
-  const bool fast = !std::getenv("CVD_GEN_GENERIC") && enc.m <= kMaxM && a.hs + 32 / std::max(enc.n, 1) <= 32;
+  return a;
+}
+
+// the bit-parallel generator applies: k <= 2 and the window of one word fits 32 bits
+bool gen_fast_ok(const CodeDesc& enc) {
+  return !std::getenv("CVD_GEN_GENERIC") && enc.m <= kMaxM && enc.k <= 2 &&
+         (enc.m + enc.k - 1) / enc.k + 32 / std::max(enc.n, 1) <= 32;
+}
+}  // namespace
+
+int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, uint64_t thr,
+                         int64_t N, int random_input, int64_t seq_base, int64_t seq_stride,
+                         uint32_t* d_r, int64_t pitch, int64_t q0, int64_t count, void* stream) {
+  if (count <= 0 || N <= 0) return CVD_OK;
+  GenArgs a = gen_args(enc, k0, k1, tag, thr, N, random_input);
+  a.seq_base = seq_base; a.seq_stride = seq_stride;
+  a.pitch = pitch; a.q0 = q0; a.count = count; a.r = d_r;
+  const unsigned grid = (unsigned)((count + kBlock - 1) / kBlock);
+  const bool fast = gen_fast_ok(enc);
   auto kern = gen_kernel<0, 0>;
   dim3 gdim(grid);
   if (fast) {
@@ -1057,6 +1196,42 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
   } else {
     hipLaunchKernelGGL(detect_table_kernel<false>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
   }
+  HIP_CHECK(hipGetLastError());
+  return CVD_OK;
+}
+
+int cvd::launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
+                         uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,
+                         int64_t* d_counts, void* stream, bool early) {
+  const int R = 1 << M.dec.n;
+  const size_t lds16 = (size_t)M.S * R * (sizeof(double) + sizeof(uint16_t)) + (R + 1) * sizeof(double);
+  const bool big = lds16 > 40 * 1024;
+  const int bs = big ? 1024 : kBlock;
+  const size_t lds = ((lds16 + 15) & ~(size_t)15) + (size_t)(bs / 64) * 128 * sizeof(uint32_t);
+  const int k = M.dec.k, n = M.dec.n;
+  if (M.kind != 0 || !M.d_rec || M.S >= 4096 || lds > 160 * 1024 || std::getenv("CVD_MC_UNFUSED") ||
+      !((k == 1 && (n == 2 || n == 3)) || (k == 2 && n == 3)) || !gen_fast_ok(e1) || !gen_fast_ok(e2) ||
+      e1.k != k || e2.k != k || e1.n != n || e2.n != n) {
+    set_error("fused trial kernel: needs an LDS-resident dense model and (k, n) in {(1,2), (1,3), (2,3)}");
+    return CVD_E_UNSUPPORTED;
+  }
+  if (T <= 0 || N <= 0) return CVD_OK;
+  FusedArgs a;
+  TabArgs& t = a.t;
+  t.rec = M.d_rec; t.logp1 = M.d_logp1; t.ltref = M.d_ltref; t.n = n;
+  t.S = M.S; t.N = N; t.nseq = 0; t.n_h1 = 0; t.r = nullptr; t.sums = d_sums; t.counts = d_counts;
+  t.early = early && !d_sums; t.lt_min = M.ltref[1]; t.lp_min = M.lp_min;
+  a.g[0] = gen_args(e1, k0, k1, tag, thr, N, 1);
+  a.g[1] = gen_args(e2, k0, k1, tag, thr, N, 1);
+  a.trial_begin = trial_begin; a.T = T; a.Tp = (T + 63) & ~(int64_t)63;
+  void (*kern)(FusedArgs) = nullptr;
+  if (k == 1 && n == 2) kern = big ? mc_table16_kernel<1, 2, 1024> : mc_table16_kernel<1, 2, kBlock>;
+  else if (k == 1 && n == 3) kern = big ? mc_table16_kernel<1, 3, 1024> : mc_table16_kernel<1, 3, kBlock>;
+  else kern = big ? mc_table16_kernel<2, 3, 1024> : mc_table16_kernel<2, 3, kBlock>;
+  if (lds > 64 * 1024)
+    HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int64_t lanes = 2 * a.Tp;
+  hipLaunchKernelGGL(kern, dim3((unsigned)((lanes + bs - 1) / bs)), dim3(bs), lds, (hipStream_t)stream, a);
   HIP_CHECK(hipGetLastError());
   return CVD_OK;
 }
@@ -1290,6 +1465,14 @@ extern "C" int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cv
   if (!(p >= 0.0 && p <= 1.0)) { set_error("p must lie in [0, 1]"); return CVD_E_INVALID; }
   const uint32_t tag = grid_tag(N, p);
   const uint64_t thr = noise_threshold(p);
+  const bool early = (path & CVD_DETECT_EARLY_DECISION) != 0;
+  if ((path & ~CVD_DETECT_EARLY_DECISION) == CVD_PATH_AUTO && model->kind == 0) {
+    // LDS-resident dense models: the fused trial kernel, no streams in HBM (same counts)
+    if ((rc = check_device(*model))) return rc;
+    rc = launch_mc_fused(*model, e1, e2, (uint32_t)seed, (uint32_t)(seed >> 32), tag, thr, N, trial_begin,
+                         trial_end - trial_begin, nullptr, d_counts, stream, early);
+    if (rc != CVD_E_UNSUPPORTED) return rc;
+  }
   uint32_t* r = static_cast<uint32_t*>(d_work);
   for (int64_t b = trial_begin; b < trial_end; b += batch) {
     const int64_t T = std::min(batch, trial_end - b);
@@ -1302,4 +1485,25 @@ extern "C" int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cv
     if ((rc = cvd_detect(model, r, N, 2 * T, T, nullptr, d_counts, path, stream))) return rc;
   }
   return CVD_OK;
+}
+
+extern "C" int cvd_mc_fused(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2, double p, int64_t N,
+                            uint64_t seed, int64_t trial_begin, int64_t trial_end, double* d_sums,
+                            int64_t* d_counts, int32_t flags, void* stream) {
+  if (!model || !d_counts || trial_end < trial_begin || N < 0) {
+    set_error("bad mc_fused arguments");
+    return CVD_E_INVALID;
+  }
+  CodeDesc e1, e2;
+  int rc;
+  if ((rc = parse_code_dev(enc1, e1)) || (rc = parse_code_dev(enc2, e2))) return rc;
+  if (!(p >= 0.0 && p <= 1.0)) { set_error("p must lie in [0, 1]"); return CVD_E_INVALID; }
+  const bool early = (flags & CVD_DETECT_EARLY_DECISION) != 0;
+  if (early && d_sums) {
+    set_error("early decision stops a trial once its decision is certain: per-trial sums need the full run");
+    return CVD_E_INVALID;
+  }
+  if ((rc = check_device(*model))) return rc;
+  return launch_mc_fused(*model, e1, e2, (uint32_t)seed, (uint32_t)(seed >> 32), grid_tag(N, p), noise_threshold(p),
+                         N, trial_begin, trial_end - trial_begin, d_sums, d_counts, stream, early);
 }

@@ -322,11 +322,15 @@ class Detector:
         return int(max(1, min(trial_count, b)))
 
     def run_trials(self, model, gen1, gen2, N, p, seed, trial_begin, trial_end, batch=None,
-                   path=_lib.PATH_AUTO, return_sums=False, counts=None, stream=None, early_decision=False):
+                   path=_lib.PATH_AUTO, return_sums=False, counts=None, stream=None, early_decision=False,
+                   fused=False):
         """Global trials [trial_begin, trial_end) of one (N, p) grid point
         (Pd_plotter.py:198-223).  Returns {"counts": (s1, s2), "sums": [T, 4]?}
         with sums per trial = (logp1, logp1_ref, logp2, logp2_ref).
-        early_decision (counts only): stop each trial once its decision is certain."""
+        early_decision (counts only): stop each trial once its decision is certain.
+        fused: generator and table automaton in one kernel (cvd_mc_fused; dense
+        LDS-resident models), sums included; the counts-only path uses it on its own
+        (cvd_mc_run, PATH_AUTO) whenever it applies."""
         if early_decision and return_sums:
             raise ValueError("early_decision gives counts only; per-trial sums need the full run")
         g1 = as_code(gen1, self.m, self.k, self.n)
@@ -336,6 +340,16 @@ class Detector:
             counts = torch.zeros(2, dtype=torch.int64, device=self.device)
         if T <= 0:
             return {"counts": counts, "sums": np.zeros((0, 4))} if return_sums else {"counts": counts}
+        if fused:
+            sums = torch.empty((T, 4), dtype=torch.float64, device=self.device) if return_sums else None
+            flags = _lib.DETECT_EARLY_DECISION if early_decision else 0
+            _lib.check(_lib.lib().cvd_mc_fused(model.handle, g1.c, g2.c, float(p), int(N),
+                                               int(seed) & 0xFFFFFFFFFFFFFFFF, int(trial_begin), int(trial_end),
+                                               ctypes.c_void_p(sums.data_ptr() if sums is not None else 0),
+                                               ctypes.c_void_p(counts.data_ptr()), flags, _stream_ptr(stream)))
+            if return_sums:
+                return {"counts": counts, "sums": sums.cpu().numpy()}
+            return {"counts": counts}
         batch = self.default_batch(N, T) if batch is None else int(batch)
         lib = _lib.lib()
         if not return_sums:

@@ -14,7 +14,8 @@
  *   viterbi_markov.simulate_markov_sequence (MISSING; called Pd_plotter.py:149,212,219)
  *                                                                                  cvd_generate (+ cvd_trace)
  *   Pd_plotter.py:106-116     log_prob_sequence                                    cvd_detect (per-sequence sums)
- *   Pd_plotter.py:198-233     trial loop, decision, Pd/Pc counting                 cvd_detect (counts) / cvd_mc_run
+ *   Pd_plotter.py:198-233     trial loop, decision, Pd/Pc counting                 cvd_detect (counts) / cvd_mc_run /
+ *                                                                                  cvd_mc_fused (generator + table in one kernel)
  *   (none: the reference is single-process)                                        cvd_allreduce_counts / cvd_comm_* (RCCL)
  *   comp_parity.py:90-128     parity_satisfaction_fraction / parity_detector       cvd_parity_detect
  *                             (parity-template baseline)
@@ -208,6 +209,18 @@ int64_t cvd_mc_workspace_bytes(const cvd_code* enc1, int64_t N, int64_t batch);
 int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2,
                double p, int64_t N, uint64_t seed, int64_t trial_begin, int64_t trial_end,
                int64_t batch, void* d_work, int64_t* d_counts, int32_t path, void* stream);
+
+/* The same grid point in ONE kernel per launch, without streams in HBM: every lane
+ * generates its own sequence's received words (cvd_generate's encoder and noise, bit
+ * for bit) and runs the LDS-resident table automaton on them (dense models with
+ * S < 4096 whose tables fit a CU's LDS; (k, n) in {(1,2), (1,3), (2,3)}; otherwise
+ * CVD_E_UNSUPPORTED).  Trial t of [trial_begin, trial_end) is sequences 2t (H1, enc1)
+ * and 2t + 1 (H2, enc2) as in cvd_mc_run, which uses this path for CVD_PATH_AUTO
+ * when it applies.  d_sums (nullable): [trial_end - trial_begin][4] doubles (log P̂1,
+ * log T_ref of H1, then of H2).  flags: CVD_DETECT_EARLY_DECISION (counts only). */
+int cvd_mc_fused(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2, double p, int64_t N,
+                 uint64_t seed, int64_t trial_begin, int64_t trial_end, double* d_sums, int64_t* d_counts,
+                 int32_t flags, void* stream);
 
 /* ---- multi-GPU: the one collective (none in the reference,
  * Pd_plotter.py:176-235 is single-process) --------------------------------

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def is_det(name):
-    return "detect" in name or "k1b" in name or "parity_kernel" in name
+    return "detect" in name or "k1b" in name or "parity_kernel" in name or "mc_table16" in name
 
 
 def is_gen(name):
@@ -143,6 +143,7 @@ def main(src, name):
         },
         "config": cfg.get("name", "m6"),
         "detector": cfg.get("detector", "markov"),
+        "fused": bool(bench["diagnostic"].get("fused", False)),
         "batch": B,
         "N": N,
     }
