@@ -48,6 +48,31 @@ CVD_HD U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0
   return U4{c0, c1, c2, c3};
 }
 
+// One Philox round of B independent blocks under the round key (k0, k1): the
+// caller advances the key (k += W) between rounds, 10 rounds in all
+template <int B>
+CVD_HD void philox_round(uint32_t (&c)[B][4], uint32_t k0, uint32_t k1) {
+  uint64_t p0[B], p1[B];
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    p0[b] = (uint64_t)kPhiloxM0 * c[b][0];
+    p1[b] = (uint64_t)kPhiloxM1 * c[b][2];
+  }
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const uint32_t hi0 = (uint32_t)(p0[b] >> 32), lo0 = (uint32_t)p0[b];
+    const uint32_t hi1 = (uint32_t)(p1[b] >> 32), lo1 = (uint32_t)p1[b];
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t n0, n2;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c[b][1]), "s"(k0));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c[b][3]), "s"(k1));
+#else
+    const uint32_t n0 = hi1 ^ c[b][1] ^ k0, n2 = hi0 ^ c[b][3] ^ k1;
+#endif
+    c[b][0] = n0; c[b][1] = lo1; c[b][2] = n2; c[b][3] = lo0;
+  }
+}
+
 // B independent Philox4x32-10 blocks under one key, advanced round by round
 // over all blocks, so that neighbouring instructions belong to different
 // blocks: each block's xor3 -> multiply dependency (a wait state on gfx950)

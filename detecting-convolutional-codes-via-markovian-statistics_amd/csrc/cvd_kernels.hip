@@ -227,28 +227,47 @@ __device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMI
 //    from the lane index in the fused kernel).
 // One word at a time (3 blocks for every lane, then single blocks while any lane is
 // undecided) costs ~3.4 blocks per word; this ~2.5.
+// noise_head's plane tests on its two Philox blocks (already computed)
+__device__ __forceinline__ void noise_head_planes(const GenArgs& a, const uint32_t (&xv)[2][4], bool live,
+                                                  uint32_t valid, uint32_t& U, uint32_t& F) {
+  const uint32_t t = a.thr_lo;
+  U = live ? valid : 0u;
+  F = 0u;
+  noise_planes4(t >> 28, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U, F);
+  noise_planes4(t >> 24, xv[1][0], xv[1][1], xv[1][2], xv[1][3], U, F);
+}
+
+// Planes 1-8 (Philox blocks 0 and 1, unconditional) of word w of the sequence whose
+// counter words are `own`: U = still undecided bits, F = flips so far (straight-line
+// VALU, so a caller can interleave it with other work)
+__device__ __forceinline__ void noise_head(const GenArgs& a, uint2 own, uint32_t w, bool live, uint32_t valid,
+                                           uint32_t& U, uint32_t& F) {
+  const uint32_t t = a.thr_lo;
+  U = live ? valid : 0u;
+  F = 0u;
+  const uint32_t k0 = a.k0, k1 = a.k1;
+  uint32_t xv[2][4];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    xv[b][0] = w * kNoiseBlocksPerWord + (uint32_t)b;
+    xv[b][1] = own.x; xv[b][2] = own.y; xv[b][3] = a.tag;
+  }
+  philox_blocks<2>(xv, k0, k1);
+  noise_planes4(t >> 28, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U, F);
+  noise_planes4(t >> 24, xv[1][0], xv[1][1], xv[1][2], xv[1][3], U, F);
+}
+
+// The straggler exchange after the heads of words w4 .. w4 + 3 (wave-collective):
+// the (lane, word) pairs with an undecided bit are compacted into consecutive lanes
+// through LDS (su, sm: 64 words each per wave); slot i computes the next two blocks
+// (8 planes) of the i-th pair and the result goes back to the owner.  seq(l): the
+// (counter word 1, counter word 2) = (seq_lo, ctr_hi(seq, noise)) of lane l's sequence,
+// for the slot lanes.
 template <typename Seq>
-__device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
-                                                 const bool (&live)[4], uint32_t valid, uint32_t (&F)[4]) {
+__device__ __forceinline__ void noise_exchange(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
+                                               uint32_t (&U)[4], uint32_t (&F)[4]) {
   const uint32_t t = a.thr_lo, lane = lane_id();
   const uint32_t nslots = a.slots - 1u < 64u ? a.slots : 64u;   // 1..64: every round makes progress
-  uint32_t U[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) { U[g] = live[g] ? valid : 0u; F[g] = 0u; }
-  const uint2 own = seq(lane);
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {   // blocks 0 and 1 of word g
-    const uint32_t k0 = a.k0, k1 = a.k1;
-    uint32_t xv[2][4];
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      xv[b][0] = (w4 + g) * kNoiseBlocksPerWord + (uint32_t)b;
-      xv[b][1] = own.x; xv[b][2] = own.y; xv[b][3] = a.tag;
-    }
-    philox_blocks<2>(xv, k0, k1);
-    noise_planes4(t >> 28, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U[g], F[g]);
-    noise_planes4(t >> 24, xv[1][0], xv[1][1], xv[1][2], xv[1][3], U[g], F[g]);
-  }
 #pragma nounroll
   for (uint32_t j = 2; j < (uint32_t)kNoiseBlocksPerWord; j += 2) {
     uint32_t slot[4], tot = 0u;
@@ -289,6 +308,26 @@ __device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, uint32_t* su,
       wave_lds_sync();
     }
   }
+}
+
+// Flip masks F[g] of the words w4 + g (g < 4) of every lane's sequence, noise_word's
+// spec (cvd_common.h) for the wave; live[g] = word exists for this lane.
+//  * Planes 1-8 (Philox blocks 0 and 1) of all four words run unconditionally.  A code
+//    bit is then still undecided with probability 2^-8, so ~12% of the wave's 256
+//    (lane, word) pairs hold one (~30).
+//  * Those pairs are compacted into consecutive lanes (noise_exchange); after 16 planes
+//    ~0.1 undecided bits are left per wave and chunk; a further pass runs only while the
+//    ballot finds one.
+// One word at a time (3 blocks for every lane, then single blocks while any lane is
+// undecided) costs ~3.4 blocks per word; this ~2.5.
+template <typename Seq>
+__device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
+                                                 const bool (&live)[4], uint32_t valid, uint32_t (&F)[4]) {
+  uint32_t U[4];
+  const uint2 own = seq(lane_id());
+#pragma unroll
+  for (int g = 0; g < 4; ++g) noise_head(a, own, w4 + g, live[g], valid, U[g], F[g]);
+  noise_exchange(a, su, sm, seq, w4, U, F);
 }
 
 // Encoder of one sequence, one received word at a time (bit-parallel, see above):
@@ -421,6 +460,26 @@ struct ChunkEncoder {
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) out4[g] = w4 + g < nwords ? encode(w4 + g, nm4[g]) : 0u;
+  }
+  // the same in two parts, so that a caller can interleave the unconditional noise
+  // blocks with other work: head(g) for g = 0..3, then finish (wave-collective)
+  __device__ void head(uint2 own, int64_t w, bool live, uint32_t& U, uint32_t& F) const {
+    noise_head(*a, own, (uint32_t)w, live, kValid, U, F);
+  }
+  template <typename Seq>
+  __device__ void finish(uint32_t* su, uint32_t* sm, Seq seq, int64_t w4, uint32_t (&U)[4], uint32_t (&F)[4],
+                         int64_t nwords, uint32_t (&out4)[4]) {
+    if (a->thr_all) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) F[g] = kValid;
+    } else if (a->thr_lo) {
+      noise_exchange(*a, su, sm, seq, (uint32_t)w4, U, F);
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) F[g] = 0u;
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) out4[g] = w4 + g < nwords ? encode(w4 + g, F[g]) : 0u;
   }
 };
 
@@ -661,24 +720,42 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
   };
   ChunkEncoder<k, n> enc;
   enc.init(&g, sid0 + 2 * (uint64_t)lane);
+  const uint2 own = seq(lane);
   const int64_t N = ta.N, nwords = (N + SPW - 1) / SPW, nchunks = (nwords + 3) / 4;
   const int64_t full = N / (4 * SPW);             // chunks whose 4 words are all full
   double lp = 0.0, lr = 0.0;
   uint32_t st = 0;                                // index of D_0 = 0 (first BFS state)
   int dec = 0;                                    // early decision (0 = open)
+  // software pipeline: the words of chunk c + 1 are generated while chunk c is walked.
+  // The unconditional noise blocks of each next word (straight-line VALU) sit in the
+  // same basic block as the walk of a current word (a chain of dependent LDS gathers),
+  // so the scheduler overlaps them; the straggler exchange and the encoder follow.
+  uint32_t wv[4], U[4], F[4];
+  if (nchunks > 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) enc.head(own, e, valid && e < nwords, U[e], F[e]);
+    enc.finish(su, sm, seq, 0, U, F, nwords, wv);
+  }
   for (int64_t c = 0; c < nchunks; ++c) {
     if (ta.early && c > 0 && (c & 1) == 0 && c <= full) {   // every 2 chunks (8 words)
       if (!dec) dec = early_decide(lp, lr, N - c * 4 * SPW, ta.lt_min, ta.lp_min);
       if (__ballot(dec == 0) == 0) break;         // the whole wave: the exchange stays collective
     }
-    bool live[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) live[e] = valid && 4 * c + e < nwords;
-    uint32_t wv[4];
-    enc.chunk(su, sm, seq, 4 * c, live, nwords, wv);
-    if (c < full) {
+    const int64_t wn = 4 * (c + 1);               // first word of the next chunk
+    const bool more = c + 1 < nchunks;            // wave-uniform
+    if (c < full && more) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
+        // walk word e of this chunk with one Philox round of the next chunk's word e
+        // after each step (the two blocks of noise_head, by hand: the scheduler keeps
+        // source order, and each step waits on its LDS gather)
+        uint32_t xv[2][4];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          xv[b][0] = (uint32_t)(wn + e) * kNoiseBlocksPerWord + (uint32_t)b;
+          xv[b][1] = own.x; xv[b][2] = own.y; xv[b][3] = g.tag;
+        }
+        uint32_t k0 = g.k0, k1 = g.k1;
         uint32_t word = wv[e];
 #pragma unroll
         for (int i = 0; i < SPW; ++i) {
@@ -688,7 +765,11 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
           lp += s_lp[idx];                        // log P̂1[i, j]   (Pd_plotter.py:213)
           lr += s_lt[rv & 15u];                   // log T_ref[i, j] (Pd_plotter.py:214)
           st = rv >> 4;
+          if (i < 10) { philox_round<2>(xv, k0, k1); k0 += kPhiloxW0; k1 += kPhiloxW1; }
         }
+#pragma unroll
+        for (int r = SPW; r < 10; ++r) { philox_round<2>(xv, k0, k1); k0 += kPhiloxW0; k1 += kPhiloxW1; }
+        noise_head_planes(g, xv, valid && wn + e < nwords, ChunkEncoder<k, n>::kValid, U[e], F[e]);
       }
     } else {
       for (int e = 0; e < 4; ++e) {
@@ -696,7 +777,12 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
         if (s0 >= N) break;
         table16_word<n>(wv[e], (int)min((int64_t)SPW, N - s0), st, lp, lr, s_rec, s_lp, s_lt);
       }
+      if (more) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) enc.head(own, wn + e, valid && wn + e < nwords, U[e], F[e]);
+      }
     }
+    if (more) enc.finish(su, sm, seq, wn, U, F, nwords, wv);
   }
   if (valid && ta.sums) { ta.sums[4 * t + 2 * h] = lp; ta.sums[4 * t + 2 * h + 1] = lr; }
   early_final(dec, lp, lr);
