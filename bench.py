@@ -100,7 +100,8 @@ def parse():
     ap.add_argument("--fused", type=int, default=-1,
                     help="dense (table-automaton) configs: generator and detector in ONE kernel per step "
                          "(cvd_mc_fused: each lane generates its own words and feeds the LDS-resident "
-                         "automaton, no streams in HBM); -1: auto = on for dense models")
+                         "automaton, no streams in HBM); -1: auto = where the library prefers it "
+                         "(cvd_model_info.mc_fused: small tables, e.g. m2)")
     ap.add_argument("--cpu-baseline", type=int, default=1,
                     help="time the C oracle port on this host (rank 0, one GPU), check Pd against it at "
                          "the config's informative point, and run the C0 demo preset on both sides")
@@ -198,7 +199,7 @@ def main():
     # stream while the detector reads buffer s%2 (both kernels of every timed
     # step run inside the timed region)
     if a.fused < 0:
-        a.fused = int(not parity and not info["kind"])
+        a.fused = int(not parity and bool(info["mc_fused"]))   # where it measured faster (cvd_model_info)
     if a.fused:
         a.overlap = 0
     if a.overlap < 0:

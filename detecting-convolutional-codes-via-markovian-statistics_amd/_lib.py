@@ -40,7 +40,7 @@ class cvd_model_info(ctypes.Structure):
                 ("learn_len_eff", ctypes.c_int64), ("hash_capacity", ctypes.c_int64),
                 ("max_probe", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("logp1_unseen", ctypes.c_double), ("explicit_kernel", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("mc_fused", ctypes.c_int32)]
 
 
 KERNEL_NAMES = {0: "none", 1: "detect_explicit_kernel (generic explicit path)",

@@ -1044,7 +1044,7 @@ extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
   info->device = Mo->device;
   info->logp1_unseen = Mo->logp1_unseen;
   info->explicit_kernel = explicit_kernel_of(*Mo);
-  info->reserved = 0;
+  info->mc_fused = mc_fused_preferred(*Mo) ? 1 : 0;
   return CVD_OK;
 }
 

@@ -91,6 +91,9 @@ int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int6
 // the whole trial loop in one kernel (generator + LDS table automaton, no streams in
 // HBM): trials [trial_begin, trial_begin + T) of one grid point; CVD_E_UNSUPPORTED if
 // the model / codes do not fit it
+// the fused kernel applies to the model and measured faster than the two-kernel
+// pipeline (small LDS tables: 256-thread blocks); cvd_mc_run's AUTO path uses it then
+bool mc_fused_preferred(const cvd_model& M);
 int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
                     uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,
                     int64_t* d_counts, void* stream, bool early);

@@ -1286,6 +1286,21 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
   return CVD_OK;
 }
 
+namespace {
+size_t lds16_bytes(const cvd_model& M) {
+  const int R = 1 << M.dec.n;
+  return (size_t)M.S * R * (sizeof(double) + sizeof(uint16_t)) + (R + 1) * sizeof(double);
+}
+}  // namespace
+
+bool cvd::mc_fused_preferred(const cvd_model& M) {
+  // C1 (m2, 256-thread blocks): 102.2M vs 96.2M trials/s; C3 (rate 2/3, S = 1,807,
+  // 1024-thread blocks, 4 waves/SIMD): 4.80M vs 5.60M (profiles/r03e/)
+  const int k = M.dec.k, n = M.dec.n;
+  return M.kind == 0 && M.S < 4096 && lds16_bytes(M) <= 40 * 1024 && gen_fast_ok(M.dec) &&
+         ((k == 1 && (n == 2 || n == 3)) || (k == 2 && n == 3)) && !std::getenv("CVD_MC_UNFUSED");
+}
+
 int cvd::launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
                          uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,
                          int64_t* d_counts, void* stream, bool early) {
@@ -1552,7 +1567,7 @@ extern "C" int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cv
   const uint32_t tag = grid_tag(N, p);
   const uint64_t thr = noise_threshold(p);
   const bool early = (path & CVD_DETECT_EARLY_DECISION) != 0;
-  if ((path & ~CVD_DETECT_EARLY_DECISION) == CVD_PATH_AUTO && model->kind == 0) {
+  if ((path & ~CVD_DETECT_EARLY_DECISION) == CVD_PATH_AUTO && mc_fused_preferred(*model)) {
     // LDS-resident dense models: the fused trial kernel, no streams in HBM (same counts)
     if ((rc = check_device(*model))) return rc;
     rc = launch_mc_fused(*model, e1, e2, (uint32_t)seed, (uint32_t)(seed >> 32), tag, thr, N, trial_begin,

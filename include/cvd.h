@@ -81,7 +81,10 @@ typedef struct cvd_model_info {
   int32_t device;          /* device holding the tables, -1 if not uploaded */
   double logp1_unseen;     /* log P̂1 of a row never visited (sparse models) */
   int32_t explicit_kernel; /* kernel CVD_PATH_EXPLICIT launches: CVD_KERNEL_* */
-  int32_t reserved;
+  int32_t mc_fused;        /* 1: cvd_mc_run (CVD_PATH_AUTO) runs the fused generator + table kernel
+                              (cvd_mc_fused) for this model: an LDS-resident table small enough for
+                              256-thread blocks (measured faster there; the 1024-thread variant of the
+                              large tables is slower than the two-kernel pipeline) */
 } cvd_model_info;
 
 #define CVD_KERNEL_NONE 0       /* explicit path unsupported for this shape */
