@@ -490,6 +490,10 @@ def run_c4(a, pkg, world, rank, local, dist):
         for ip, p in enumerate(p_grid):
             det.run_trials(models[p], cc["gen1"], cc["gen2"], N, p, a.seed, lo, hi, batch=B,
                            counts=counts[iN, ip], early_decision=False)
+            if N >= 100_000:   # a progress line per long grid point (the launches are queued)
+                torch.cuda.synchronize()
+                print(json.dumps({"c4_point": {"rank": rank, "N": N, "p": p, "seconds": time.perf_counter() - tn}}),
+                      file=sys.stderr, flush=True)
         torch.cuda.synchronize()
         per_n_s.append(time.perf_counter() - tn)
         print(json.dumps({"c4_progress": {"rank": rank, "N": N, "seconds": per_n_s[-1]}}), file=sys.stderr,

@@ -584,39 +584,77 @@ __global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
   count_decisions(valid, q < a.n_h1, lp, lr, a.counts);
 }
 
-// Enumerated automaton with the whole model LDS-resident (S < 4096 and
-// S*2^n*(8 + 2) + (2^n + 1)*8 bytes within the 160 KiB of a CU): records as
-// 16-bit next << 4 | c, log P̂1 as f64.  Per step one u16 and two f64 LDS
-// gathers; the only dependent chain is the u16 record (next state).  The
-// received words are read in 16-byte chunks one chunk ahead (64 or 40 steps
-// of lead), and full chunks run fully unrolled.
-template <int n>
-__device__ __forceinline__ void table16_word(uint32_t word, int ns, uint32_t& st, double& lp, double& lr,
-                                             const uint16_t* s_rec, const double* s_lp, const double* s_lt) {
-  constexpr uint32_t R = 1u << n;
-  for (int i = 0; i < ns; ++i) {
-    const uint32_t idx = st * R + (word & (R - 1u));
-    word >>= n;
-    const uint32_t e = s_rec[idx];
-    lp += s_lp[idx];                   // log P̂1[i, j]   (Pd_plotter.py:213)
-    lr += s_lt[e & 15u];               // log T_ref[i, j] = log(c / 2^n) (Pd_plotter.py:214)
-    st = e >> 4;
+// Enumerated automaton with the whole model LDS-resident (S < 4096 and its image
+// within the 160 KiB of a CU).  Two images (LdsModel):
+//  * kLr = false (any table that fits): log P̂1 as f64 [S 2^n], log T_ref(c) f64
+//    [2^n + 1], records 16-bit next << 4 | c [S 2^n] -- 10 B per entry.  Per step one
+//    u16 and two f64 gathers, and the index math of next * 2^n + r, c * 8 and the
+//    shifts (~40 issue cycles of VALU per step, measured by the ISA: the walk is
+//    VALU-bound, not LDS-bound).
+//  * kLr = true (small tables, S 2^n 18 B <= 32 KiB: m2, m3): log P̂1 and log T_ref(i,
+//    r) = ltref[c] as two f64 arrays [S 2^n] and 16-bit next * 2^n, the next state's
+//    entry base -- 18 B per entry, built from the same device arrays at kernel start.
+//    Per step one bit-field extract, one add, two address shift-adds, one add and the
+//    two f64 adds (~27 issue cycles), the same three gathers.
+// The only dependent chain is the u16 record (next state).  The received words are
+// read in 16-byte chunks one chunk ahead (64 or 40 steps of lead), and full chunks run
+// fully unrolled.
+template <int n, bool kLr>
+struct LdsModel {
+  static constexpr uint32_t R = 1u << n;
+  const double* lp;      // [SR] log P̂1
+  const double* lt;      // kLr: [SR] log T_ref(i, r); else [R + 1] log(c / 2^n)
+  const uint16_t* rec;   // kLr: [SR] next * 2^n; else [SR] next << 4 | c
+  __host__ __device__ static size_t bytes(int64_t SR) {
+    return kLr ? (size_t)SR * 18 : (size_t)SR * 10 + (R + 1) * sizeof(double);
   }
-}
+  __device__ void fill(const TabArgs& a, char* smem, int BS) {
+    const int SR = (int)a.S * (int)R;
+    double* s_lp = reinterpret_cast<double*>(smem);
+    double* s_lt = s_lp + SR;
+    uint16_t* s_rec = reinterpret_cast<uint16_t*>(s_lt + (kLr ? SR : (int)R + 1));
+    for (int i = threadIdx.x; i < SR; i += BS) {
+      const uint32_t e = a.rec[i];
+      s_lp[i] = a.logp1[i];
+      if constexpr (kLr) {
+        s_lt[i] = a.ltref[e & 15u];
+        s_rec[i] = (uint16_t)((e >> 4) * R);   // S * 2^n < 65536 (host-checked)
+      } else {
+        s_rec[i] = (uint16_t)e;                // next < 4096: next << 4 | c fits 16 bits (host-checked)
+      }
+    }
+    if constexpr (!kLr)
+      for (int i = threadIdx.x; i <= (int)R; i += BS) s_lt[i] = a.ltref[i];
+    lp = s_lp; lt = s_lt; rec = s_rec;
+  }
+  // st: the state's entry base (kLr) or index; state 0 is 0 either way
+  __device__ __forceinline__ void step(uint32_t& st, uint32_t r, double& lps, double& lrs) const {
+    if constexpr (kLr) {
+      const uint32_t idx = st + r;
+      const uint32_t nx = rec[idx];
+      lps += lp[idx];                 // log P̂1[i, j]   (Pd_plotter.py:213)
+      lrs += lt[idx];                 // log T_ref[i, j] (Pd_plotter.py:214)
+      st = nx;
+    } else {
+      const uint32_t idx = st * R + r;
+      const uint32_t e = rec[idx];
+      lps += lp[idx];                 // log P̂1[i, j]   (Pd_plotter.py:213)
+      lrs += lt[e & 15u];             // log T_ref[i, j] = log(c / 2^n) (Pd_plotter.py:214)
+      st = e >> 4;
+    }
+  }
+  // the first ns steps of a word (step i in bits n*i .. n*i + n - 1)
+  __device__ __forceinline__ void word(uint32_t w, int ns, uint32_t& st, double& lps, double& lrs) const {
+    for (int i = 0; i < ns; ++i) step(st, __builtin_amdgcn_ubfe(w, (uint32_t)(n * i), (uint32_t)n), lps, lrs);
+  }
+};
 
-template <int n, int BS>
+template <int n, int BS, bool kLr>
 __global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
-  constexpr int R = 1 << n, SPW = 32 / n;
+  constexpr int SPW = 32 / n;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int SR = (int)a.S * R;
-  double* s_lp = reinterpret_cast<double*>(smem);
-  double* s_lt = s_lp + SR;
-  uint16_t* s_rec = reinterpret_cast<uint16_t*>(s_lt + R + 1);
-  for (int i = threadIdx.x; i < SR; i += BS) {
-    s_lp[i] = a.logp1[i];
-    s_rec[i] = (uint16_t)a.rec[i];     // next < 4096: next << 4 | c fits 16 bits (host-checked)
-  }
-  for (int i = threadIdx.x; i <= R; i += BS) s_lt[i] = a.ltref[i];
+  LdsModel<n, kLr> md;
+  md.fill(a, smem, BS);
   __syncthreads();
   const int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x;
   const bool valid = q < a.nseq;
@@ -629,7 +667,7 @@ __global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
     uint4 cur = make_uint4(0u, 0u, 0u, 0u), nxt = cur;
     if (nchunks > 0) cur = rc[0];
     if (nchunks > 1) nxt = rc[cs];
-    uint32_t st = 0;                              // index of D_0 = 0 (first BFS state)
+    uint32_t st = 0;                              // D_0 = 0 (first BFS state)
     int dec = 0;                                  // early decision (0 = open)
     for (int64_t c = 0; c < nchunks; ++c) {
       if (a.early && c > 0 && (c & 1) == 0 && c <= full) {   // every 2 chunks (8 words)
@@ -643,22 +681,15 @@ __global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
       if (c < full) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          uint32_t word = wv[e];
 #pragma unroll
-          for (int i = 0; i < SPW; ++i) {
-            const uint32_t idx = st * (uint32_t)R + (word & (uint32_t)(R - 1));
-            word >>= n;
-            const uint32_t rv = s_rec[idx];
-            lp += s_lp[idx];
-            lr += s_lt[rv & 15u];
-            st = rv >> 4;
-          }
+          for (int i = 0; i < SPW; ++i)
+            md.step(st, __builtin_amdgcn_ubfe(wv[e], (uint32_t)(n * i), (uint32_t)n), lp, lr);
         }
       } else {
         for (int e = 0; e < 4; ++e) {
           const int64_t t0 = (4 * c + e) * SPW;
           if (t0 >= N) break;
-          table16_word<n>(wv[e], (int)min((int64_t)SPW, N - t0), st, lp, lr, s_rec, s_lp, s_lt);
+          md.word(wv[e], (int)min((int64_t)SPW, N - t0), st, lp, lr);
         }
       }
     }
@@ -686,22 +717,15 @@ struct FusedArgs {
   int64_t trial_begin, T, Tp;
 };
 
-template <int k, int n, int BS>
+template <int k, int n, int BS, bool kLr>
 __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
-  constexpr int R = 1 << n, SPW = 32 / n;
+  constexpr int SPW = 32 / n;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const TabArgs& ta = a.t;
-  const int SR = (int)ta.S * R;
-  double* s_lp = reinterpret_cast<double*>(smem);
-  double* s_lt = s_lp + SR;
-  uint16_t* s_rec = reinterpret_cast<uint16_t*>(s_lt + R + 1);
+  LdsModel<n, kLr> md;
+  md.fill(ta, smem, BS);
   // the noise exchange's slot records, 2 x 64 words per wave, after the model
-  uint32_t* s_x = reinterpret_cast<uint32_t*>(smem + (((size_t)SR * 10 + (R + 1) * 8 + 15) & ~(size_t)15));
-  for (int i = threadIdx.x; i < SR; i += BS) {
-    s_lp[i] = ta.logp1[i];
-    s_rec[i] = (uint16_t)ta.rec[i];    // next < 4096: next << 4 | c fits 16 bits (host-checked)
-  }
-  for (int i = threadIdx.x; i <= R; i += BS) s_lt[i] = ta.ltref[i];
+  uint32_t* s_x = reinterpret_cast<uint32_t*>(smem + ((LdsModel<n, kLr>::bytes(ta.S * (1 << n)) + 15) & ~(size_t)15));
   __syncthreads();
   uint32_t* su = s_x + (threadIdx.x / 64) * 128;
   uint32_t* sm = su + 64;
@@ -724,7 +748,7 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
   const int64_t N = ta.N, nwords = (N + SPW - 1) / SPW, nchunks = (nwords + 3) / 4;
   const int64_t full = N / (4 * SPW);             // chunks whose 4 words are all full
   double lp = 0.0, lr = 0.0;
-  uint32_t st = 0;                                // index of D_0 = 0 (first BFS state)
+  uint32_t st = 0;                                // D_0 = 0 (first BFS state)
   int dec = 0;                                    // early decision (0 = open)
   // software pipeline: the words of chunk c + 1 are generated while chunk c is walked.
   // The unconditional noise blocks of each next word (straight-line VALU) sit in the
@@ -759,12 +783,7 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
         uint32_t word = wv[e];
 #pragma unroll
         for (int i = 0; i < SPW; ++i) {
-          const uint32_t idx = st * (uint32_t)R + (word & (uint32_t)(R - 1));
-          word >>= n;
-          const uint32_t rv = s_rec[idx];
-          lp += s_lp[idx];                        // log P̂1[i, j]   (Pd_plotter.py:213)
-          lr += s_lt[rv & 15u];                   // log T_ref[i, j] (Pd_plotter.py:214)
-          st = rv >> 4;
+          md.step(st, __builtin_amdgcn_ubfe(word, (uint32_t)(n * i), (uint32_t)n), lp, lr);
           if (i < 10) { philox_round<2>(xv, k0, k1); k0 += kPhiloxW0; k1 += kPhiloxW1; }
         }
 #pragma unroll
@@ -775,7 +794,7 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
       for (int e = 0; e < 4; ++e) {
         const int64_t s0 = (4 * c + e) * SPW;
         if (s0 >= N) break;
-        table16_word<n>(wv[e], (int)min((int64_t)SPW, N - s0), st, lp, lr, s_rec, s_lp, s_lt);
+        md.word(wv[e], (int)min((int64_t)SPW, N - s0), st, lp, lr);
       }
       if (more) {
 #pragma unroll
@@ -1252,6 +1271,14 @@ int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t
   return CVD_OK;
 }
 
+namespace {
+// the small-table LDS image (LdsModel kLr): S 2^n 18 B <= 32 KiB, 256-thread blocks
+bool table_lr(const cvd_model& M) {
+  const int64_t SR = M.S * ((int64_t)1 << M.dec.n);
+  return SR * 18 <= 32 * 1024 && !std::getenv("CVD_TABLE_NOLR");
+}
+}  // namespace
+
 int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                              int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream, bool early) {
   if (M.kind != 0 || !M.d_rec) { set_error("table path needs a dense (enumerated) model"); return CVD_E_UNSUPPORTED; }
@@ -1269,11 +1296,16 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
   if (M.S < 4096 && lds16 <= 160 * 1024 && (M.dec.n == 2 || M.dec.n == 3) && !std::getenv("CVD_TABLE_WIDE")) {
     const bool big = lds16 > 40 * 1024;
     const int bs = big ? 1024 : kBlock;
-    void (*kern)(TabArgs) = M.dec.n == 2 ? (big ? detect_table16_kernel<2, 1024> : detect_table16_kernel<2, kBlock>)
-                                         : (big ? detect_table16_kernel<3, 1024> : detect_table16_kernel<3, kBlock>);
-    if (lds16 > 64 * 1024)
-      HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds16));
-    hipLaunchKernelGGL(kern, dim3((unsigned)((nseq + bs - 1) / bs)), dim3(bs), lds16, (hipStream_t)stream, a);
+    const bool lr = table_lr(M);
+    const size_t lds = lr ? (size_t)M.S * R * 18 : lds16;
+    void (*kern)(TabArgs) =
+        M.dec.n == 2 ? (big ? detect_table16_kernel<2, 1024, false>
+                            : lr ? detect_table16_kernel<2, kBlock, true> : detect_table16_kernel<2, kBlock, false>)
+                     : (big ? detect_table16_kernel<3, 1024, false>
+                            : lr ? detect_table16_kernel<3, kBlock, true> : detect_table16_kernel<3, kBlock, false>);
+    if (lds > 64 * 1024)
+      HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, dim3((unsigned)((nseq + bs - 1) / bs)), dim3(bs), lds, (hipStream_t)stream, a);
     HIP_CHECK(hipGetLastError());
     return CVD_OK;
   }
@@ -1308,7 +1340,9 @@ int cvd::launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc&
   const size_t lds16 = (size_t)M.S * R * (sizeof(double) + sizeof(uint16_t)) + (R + 1) * sizeof(double);
   const bool big = lds16 > 40 * 1024;
   const int bs = big ? 1024 : kBlock;
-  const size_t lds = ((lds16 + 15) & ~(size_t)15) + (size_t)(bs / 64) * 128 * sizeof(uint32_t);
+  const bool lr = !big && table_lr(M);
+  const size_t limg = lr ? (size_t)M.S * R * 18 : lds16;
+  const size_t lds = ((limg + 15) & ~(size_t)15) + (size_t)(bs / 64) * 128 * sizeof(uint32_t);
   const int k = M.dec.k, n = M.dec.n;
   if (M.kind != 0 || !M.d_rec || M.S >= 4096 || lds > 160 * 1024 || std::getenv("CVD_MC_UNFUSED") ||
       !((k == 1 && (n == 2 || n == 3)) || (k == 2 && n == 3)) || !gen_fast_ok(e1) || !gen_fast_ok(e2) ||
@@ -1326,9 +1360,15 @@ int cvd::launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc&
   a.g[1] = gen_args(e2, k0, k1, tag, thr, N, 1);
   a.trial_begin = trial_begin; a.T = T; a.Tp = (T + 63) & ~(int64_t)63;
   void (*kern)(FusedArgs) = nullptr;
-  if (k == 1 && n == 2) kern = big ? mc_table16_kernel<1, 2, 1024> : mc_table16_kernel<1, 2, kBlock>;
-  else if (k == 1 && n == 3) kern = big ? mc_table16_kernel<1, 3, 1024> : mc_table16_kernel<1, 3, kBlock>;
-  else kern = big ? mc_table16_kernel<2, 3, 1024> : mc_table16_kernel<2, 3, kBlock>;
+  if (k == 1 && n == 2)
+    kern = big ? mc_table16_kernel<1, 2, 1024, false> : lr ? mc_table16_kernel<1, 2, kBlock, true>
+                                                         : mc_table16_kernel<1, 2, kBlock, false>;
+  else if (k == 1 && n == 3)
+    kern = big ? mc_table16_kernel<1, 3, 1024, false> : lr ? mc_table16_kernel<1, 3, kBlock, true>
+                                                         : mc_table16_kernel<1, 3, kBlock, false>;
+  else
+    kern = big ? mc_table16_kernel<2, 3, 1024, false> : lr ? mc_table16_kernel<2, 3, kBlock, true>
+                                                         : mc_table16_kernel<2, 3, kBlock, false>;
   if (lds > 64 * 1024)
     HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int64_t lanes = 2 * a.Tp;
