@@ -1296,13 +1296,13 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
   if (M.S < 4096 && lds16 <= 160 * 1024 && (M.dec.n == 2 || M.dec.n == 3) && !std::getenv("CVD_TABLE_WIDE")) {
     const bool big = lds16 > 40 * 1024;
     const int bs = big ? 1024 : kBlock;
-    const bool lr = table_lr(M);
-    const size_t lds = lr ? (size_t)M.S * R * 18 : lds16;
-    void (*kern)(TabArgs) =
-        M.dec.n == 2 ? (big ? detect_table16_kernel<2, 1024, false>
-                            : lr ? detect_table16_kernel<2, kBlock, true> : detect_table16_kernel<2, kBlock, false>)
-                     : (big ? detect_table16_kernel<3, 1024, false>
-                            : lr ? detect_table16_kernel<3, kBlock, true> : detect_table16_kernel<3, kBlock, false>);
+    // (the small-table image measured slower here: in the LDS-bound stand-alone walk its
+    // log T_ref gathers spread over S 2^n entries instead of 2^n + 1 broadcast ones --
+    // m2 overlapped step 43.6 -> 47.2 ms, profiles/r03f/; the fused kernel, VALU-bound,
+    // gains from it)
+    const size_t lds = lds16;
+    void (*kern)(TabArgs) = M.dec.n == 2 ? (big ? detect_table16_kernel<2, 1024, false> : detect_table16_kernel<2, kBlock, false>)
+                                         : (big ? detect_table16_kernel<3, 1024, false> : detect_table16_kernel<3, kBlock, false>);
     if (lds > 64 * 1024)
       HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)((nseq + bs - 1) / bs)), dim3(bs), lds, (hipStream_t)stream, a);
