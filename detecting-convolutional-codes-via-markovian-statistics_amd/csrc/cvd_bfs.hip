@@ -400,7 +400,6 @@ extern "C" int cvd_enumerate_device(const cvd_code* dec, int32_t device, int64_t
   int32_t nlev = 0;
   if (level_sizes && max_levels > 0) level_sizes[0] = 1;
   nlev = 1;
-  int rc = CVD_OK;
   const bool verbose = std::getenv("CVD_BFS_VERBOSE") != nullptr;
   const double tlimit = (double)env_i64("CVD_BFS_SECONDS", 0);
   const auto t_start = std::chrono::steady_clock::now();
@@ -502,6 +501,5 @@ extern "C" int cvd_enumerate_device(const cvd_code* dec, int32_t device, int64_t
         }
     }
   }
-  (void)rc;
   return CVD_OK;
 }
