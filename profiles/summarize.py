@@ -68,7 +68,10 @@ def main(src, name):
     ms_by_p = bench["diagnostic"].get("detector_ms_by_p", {})
 
     def derive(c, ms=None):
-        waves = c.get("SQ_WAVES", 2 * B / 64)
+        # per wave-step figures over the launch's own waves (2 B sequences, 64 per wave):
+        # the SQ_WAVES counter of a pass can include a few waves of a neighbouring
+        # kernel (the last launch of profiles/r03h_m6: 86,012 for 81,920)
+        waves = 2 * B / 64
         raw = c.get("FETCH_SIZE", 0.0) * 1024
         # The guide's x2 (FETCH_SIZE = half of a 16-B/lane streaming read) applies to the
         # stream chunks only: they are the algorithmic bytes, read once as 16-B lane loads,
@@ -96,7 +99,7 @@ def main(src, name):
     keys = set().union(*[set(v["counters_per_launch"]) for v in per_p.values()]) if per_p else set()
     per = {k: sum(v["counters_per_launch"].get(k, 0.0) for v in per_p.values()) / max(1, len(per_p)) for k in keys}
     sweep = derive(per)
-    waves = per.get("SQ_WAVES", 2 * B / 64)
+    waves = 2 * B / 64
     kernel_cycles = sweep["kernel_cycles"]
     gen = {}
     for tag, disp in gen_rows.items():
