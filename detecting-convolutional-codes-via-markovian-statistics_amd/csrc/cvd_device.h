@@ -137,6 +137,8 @@ struct ExpArgs {
   const uint32_t* hkey;     // [hcap][NW] nibble-packed metric vectors, word 0 = kEmptyKey if empty
   const uint32_t* hrow;     // [hcap][row_words(n)]: per r, {log P̂1[r] (f64), successor row[r] (i32, -1 = not a row), pad}
   const uint32_t* drow;     // [rows][row_words(n)]: the same records dense by row id (table mode)
+  const uint32_t* dkey;     // [rows][NW]: the key of every learned row by row id (k1b_walk: a lane leaving
+                            // a table walk rebuilds its metric vector from it)
   const double* ltref;      // [R + 1]
   const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
@@ -153,6 +155,8 @@ struct ExpArgs {
   int64_t* counts;
   uint8_t* trace;
   int32_t early;            // early decision (counts only; sums == nullptr)
+  int32_t walk;             // k1b_walk for H1 waves (specialised kernel; no trace, no early decision, N < 2^31)
+  int32_t walk_wmin, walk_amin, walk_burst;   // k1b_walk schedule (see there)
   double lt_min, lp_min;    // smallest log T_ref / log P̂1 increments (early_decide)
 };
 
@@ -238,19 +242,32 @@ struct RowCursor {
   uint32_t hs, fb, fw, fb1, fw1;   // filter block words and their patterns
   bool cand;
   double plp;
+  uint32_t pc;                     // T_ref count c of the entry (kC loads only: the walk mode of k1b_walk)
   uint32_t pkey[NW];
-  // record entry r (log P̂1[r], successor row[r]: 16 bytes, one 12-byte load) of
-  // row s (dense records, table mode) or of directory slot s (a hashed lookup's
-  // hit) for word rn; the asm keeps the address one shift-add of the lane's word
-  // onto the record offset
+  // record entry r (log P̂1[r], successor row[r], T_ref count c: 16 bytes, one
+  // 12-byte load, 16 with kC) of row s (dense records, table mode) or of directory
+  // slot s (a hashed lookup's hit) for word rn; the asm keeps the address one
+  // shift-add of the lane's word onto the record offset
+  template <bool kC = false>
   __device__ void load_entry(const uint32_t* base, uint32_t off, uint32_t rn) {
     uint32_t o;
     asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o) : "v"(rn), "v"(off));
-    const uint3 v = ld_off<uint3>(base, o);
-    plp = __hiloint2double((int)v.y, (int)v.x);
-    pnx = (int32_t)v.z;
+    if constexpr (kC) {
+      // (plp last: a trailing 32-bit store here and the filter words' in prefetch's
+      // hashed branch get sunk into one store through a pointer phi, which keeps pc
+      // and fw1 in scratch)
+      const uint4 v = ld_off<uint4>(base, o);
+      pc = v.w;
+      pnx = (int32_t)v.z;
+      plp = __hiloint2double((int)v.y, (int)v.x);
+    } else {
+      const uint3 v = ld_off<uint3>(base, o);
+      plp = __hiloint2double((int)v.y, (int)v.x);
+      pnx = (int32_t)v.z;
+    }
   }
-  __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) { load_entry(a.drow, (uint32_t)s * RSB, rn); }
+  template <bool kC = false>
+  __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) { load_entry<kC>(a.drow, (uint32_t)s * RSB, rn); }
   __device__ void prefetch_dir(const ExpArgs& a, int32_t s, uint32_t rn) { load_entry(a.hrow, (uint32_t)s << a.rsh, rn); }
   __device__ void start(const ExpArgs& a, uint32_t r0) {
     // (CVD_ABL & 4: a pattern no filter word passes, so no lane ever becomes a candidate)
@@ -368,12 +385,12 @@ struct RowCursor {
   // D_t's key is known: issue the next step's loads
   // kmu8: the key's offset c * 0x11111111, c in {kLo, kLo + 1}
   // hi: the offset is kLo + 1 (else kLo), as a flag the caller already has
-  template <int kLo = 0>
+  template <int kLo = 0, bool kC = false>
   __device__ void prefetch(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t rn, uint32_t kmu8 = 0u,
                            bool hi = false) {
     if (CVD_ABL & 1) return;
     if (slot >= 0) {
-      prefetch_row(a, slot, rn);
+      prefetch_row<kC>(a, slot, rn);
     } else if (slot == -2 && !(CVD_ABL & 4)) {
       uint32_t ph, pl;
       cvd::key_hash_less<kLo>(key_in, NW, kLo + (hi ? 1u : 0u), ph, pl);   // = key_hash(key_in - kmu8)
@@ -624,6 +641,203 @@ struct IntC {
   static constexpr int value = V;
 };
 
+// ──────── H1 waves that walk learned rows (k1b_walk; specialised kernel) ────────
+//
+// An H1 sequence (encoder G1, the decoder's own code) spends most of its steps in
+// learned rows at small p (rows hold D_t for 98% of the steps at p = 0.01, 96% at
+// 0.02, 75% at 0.05, 24% at 0.1, <= 3% at p >= 0.15; m = 6, learn_len 10^6): there
+// the successor row, log P̂1 and the T_ref count c of every step are in the row's
+// record, and the metric vector is not needed.  The lockstep body still runs the
+// whole ACS for such a lane, since its wave's other lanes need it.  Here the lanes
+// of an H1 wave keep their own step counts and are in one of four modes:
+//   WALK  D_{t-1} is learned row `slot`, its entry for r_t loaded (log P̂1,
+//         successor, c): a walk step adds both logs and moves to the successor --
+//         one dependent 16-byte load, a dozen VALU, no ACS;
+//   PEND  the entry's successor is not a row: the lane needs D_t = ACS(D_{t-1}, r_t)
+//         and has started the load of row `slot`'s key (a.dkey) to rebuild its
+//         metric vector;
+//   ACS   metric vector valid: an ACS step as in k1b_body; a lane whose D_t is a row
+//         (successor or hashed hit) goes back to WALK;
+//   DONE  t = N.
+// The wave alternates walk bursts (up to walk_burst steps of every WALK lane) and
+// ACS steps (every PEND / ACS lane), choosing a burst when some lane walks and
+// either no lane needs the ACS, or >= walk_wmin lanes walk, or < walk_amin lanes
+// need it.  Every iteration moves some lane forward, so the loop ends.  The ACS
+// kinds alternate per ACS step of the wave (the layout is the wave's, not the
+// lane's), and a PEND lane's vector is rebuilt in the layout of the coming kind with
+// mu_prev = 0 (pairs = D + 1).  Per-trial sums are the lockstep body's bit for bit:
+// each lane adds the same terms in step order.
+enum : uint32_t { kWalkAcs = 0u, kWalkPend = 1u, kWalkWalk = 2u, kWalkDone = 3u };
+
+template <int m, uint64_t XM>
+__device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64_t vmask, const double* s_lt) {
+  constexpr int M = 1 << m, H = M / 2, NW = M / 8, R = 4;
+  const bool valid = qwave + lane_id() < a.nseq;
+  const uint32_t N = (uint32_t)a.N;
+  const uint32_t nwords = (N + 15u) / 16u;
+  const size_t cstride = (size_t)a.nseq * 4;
+  // received words: the lane's words pos / 16 (curw) and pos / 16 + 1 (nxtw); a lane
+  // that moves into nxtw reloads it at the top of the next iteration (need), not
+  // inside a walk burst: loads complete in issue order, so a word load issued there
+  // would hold up every later record load of the burst (walk_burst <= 16: a lane
+  // crosses at most one word per iteration)
+  auto load_word = [&](uint32_t wi) -> uint32_t {
+    if (wi >= nwords) return 0u;
+    return a.r[(size_t)(wi >> 2) * cstride + (size_t)(qwave + lane_id()) * 4 + (wi & 3u)];
+  };
+  uint32_t pos = 0u, curw = 0u, nxtw = 0u;
+  bool need = false;
+  // bits 0-1: r of step pos + 1
+  auto word_at = [&]() -> uint32_t { return curw >> (2u * (pos & 15u)); };
+  auto advance = [&]() {
+    ++pos;
+    if ((pos & 15u) == 0u) {
+      curw = nxtw;
+      need = true;
+    }
+  };
+  uint32_t Dp[H];
+  uint32_t key[NW];
+#pragma unroll
+  for (int i = 0; i < H; ++i) Dp[i] = 0x00010001u;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) key[w] = 0x11111111u;
+  uint32_t kmu8 = 0x11111111u, mu_prev = 0u;
+  double lp = 0.0, lr = 0.0;
+  RowCursor<NW, R> cur;
+  cur.slot = -1; cur.pnx = -1; cur.hs = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u;
+  cur.cand = false; cur.plp = 0.0; cur.pc = 1u;
+  uint32_t mode = kWalkDone;
+  if (valid && N > 0u) {
+    curw = load_word(0u);
+    nxtw = load_word(1u);
+    cur.slot = a.slot0;   // D_0 = 0 is a learned row: every lane starts walking
+    cur.template prefetch_row<true>(a, cur.slot, curw & 3u);
+    mode = kWalkWalk;
+  }
+  // Before an ACS step with PEND lanes: every lane's pairs from a canonical key (no
+  // divergent write, so the pairs keep their registers).  A PEND lane's is row
+  // `slot`'s key (parked in Dp[0, NW): its pairs are dead); an ACS lane's is its own
+  // D_{t-1} (key - kmu8), so its vector is only re-expressed.  Pairs in the layout the
+  // coming ACS kind reads (L 0: (D(2i), D(2i+1)); L 1: (D(x), D(x+2)), x = 4(i >> 1) +
+  // (i & 1)) as D + 1 (mu_prev = 0), and the lazy key D + 1.
+  auto unpack = [&](auto lay) {
+    constexpr int L = decltype(lay)::value;
+    const bool pend = mode == kWalkPend;
+    uint32_t lo[NW], hi[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint32_t k = (pend ? Dp[w] : key[w] - kmu8) + 0x11111111u;
+      key[w] = k;
+      lo[w] = k & 0x0F0F0F0Fu;           // nibbles 0, 2, 4, 6 as bytes 0..3
+      hi[w] = (k >> 4) & 0x0F0F0F0Fu;    // nibbles 1, 3, 5, 7
+    }
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      const int s0 = L == 0 ? 2 * i : 4 * (i >> 1) + (i & 1), s1 = L == 0 ? s0 + 1 : s0 + 2;
+      const int n0 = cvd::key_nibble(M, s0), n1 = cvd::key_nibble(M, s1);
+      const uint32_t b0 = (n0 & 1) ? 4u + (uint32_t)(n0 >> 1) : (uint32_t)(n0 >> 1);
+      const uint32_t b1 = (n1 & 1) ? 4u + (uint32_t)(n1 >> 1) : (uint32_t)(n1 >> 1);
+      Dp[i] = __builtin_amdgcn_perm(hi[s0 >> 3], lo[s0 >> 3], b0 | (0x0Cu << 8) | (b1 << 16) | (0x0Cu << 24));
+    }
+    kmu8 = 0x11111111u;
+    mu_prev = 0u;
+    if (pend) mode = kWalkAcs;
+  };
+  // one ACS step of the wave (every lane computes; ACS lanes keep the result)
+  auto acs_step = [&](auto kind) {
+    constexpr int KIND = decltype(kind)::value;
+    const uint32_t rr = word_at() & 3u;
+    uint32_t kw[NW];
+    uint32_t zn = 0u;
+    k1b_acs<m, true, XM, KIND>(a, nullptr, cur, rr, Dp, kw, 0u, 0u, zn, mu_prev);
+    const uint32_t mu = (zn & 0x88888888u) == 0u;
+    const uint32_t off8 = mu ? 0x22222222u : 0x11111111u;
+    if (mode == kWalkAcs) {
+      cur.fence(zn);
+      cur.template fence_keys<NW>(zn);
+      lp += cur.resolve(a, key, rr, kmu8);   // Pd_plotter.py:115, T = P̂1
+      constexpr int NH = NW / 2;
+      const uint32_t pm = (uint32_t)__builtin_amdgcn_sbfe(6, rr, 1);
+      uint32_t hx = 0u, sym = 0u;
+      constexpr bool kUni = xm_uni<m, XM>();
+#pragma unroll
+      for (int v = 0; v < NH; ++v) {
+        const uint32_t dh = key[v] ^ key[v + NH];
+        if (kUni) hx |= dh;
+        sym |= dh & (xm_even<m, XM>(v) ^ pm);
+      }
+      const uint32_t c = 1u + (sym == 0u) + ((kUni && hx == 0u) ? 2u : 0u);
+      lr += s_lt[c];                         // Pd_plotter.py:115, T = T_ref(1/2)
+#pragma unroll
+      for (int v = 0; v < NW; ++v) key[v] = kw[v];
+      kmu8 = off8;
+      mu_prev = mu;
+      advance();
+      if (pos == N) {
+        mode = kWalkDone;
+        cur.slot = -1;
+      } else {
+        cur.template prefetch<1, true>(a, key, word_at() & 3u, kmu8, mu != 0u);
+        if (cur.slot >= 0) mode = kWalkWalk;
+      }
+    }
+  };
+  const uint32_t wmin = (uint32_t)a.walk_wmin, amin = (uint32_t)a.walk_amin;
+  const int burst = a.walk_burst;
+  // every iteration moves a lane a step or out of a walk: 2 (N + 1) per lane bound it
+  // (a guard only: the loop ends by itself)
+  for (int64_t it = 0, it_max = 128 * ((int64_t)N + 1); it < it_max; ++it) {
+    if (need) {
+      nxtw = load_word((pos >> 4) + 1u);
+      need = false;
+    }
+    const uint64_t mA = __ballot(mode <= kWalkPend), mW = __ballot(mode == kWalkWalk);
+    if ((mA | mW) == 0u) break;
+    const uint32_t nA = (uint32_t)__popcll(mA), nW = (uint32_t)__popcll(mW);
+    if (nW != 0u && (nA == 0u || nW >= wmin || nA < amin)) {
+      for (int b = 0; b < burst; ++b) {
+        if (mode == kWalkWalk) {
+          if (cur.pnx < 0) {
+            // D_t is not a row: rebuild D_{t-1} (row `slot`) for the ACS
+            mode = kWalkPend;
+            const uint32_t* kp = a.dkey + (size_t)cur.slot * NW;
+#pragma unroll
+            for (int i = 0; i < NW / 4; ++i) {
+              const uint4 v = *reinterpret_cast<const uint4*>(kp + 4 * i);
+              Dp[4 * i] = v.x; Dp[4 * i + 1] = v.y; Dp[4 * i + 2] = v.z; Dp[4 * i + 3] = v.w;
+            }
+          } else {
+            lp += cur.plp;                   // Pd_plotter.py:115, from the row's record
+            lr += s_lt[cur.pc];
+            cur.slot = cur.pnx;
+            advance();
+            if (pos == N) {
+              mode = kWalkDone;
+              cur.slot = -1;
+            } else {
+              cur.template prefetch_row<true>(a, cur.slot, word_at() & 3u);
+            }
+          }
+        }
+        if (__ballot(mode == kWalkWalk) == 0u) break;
+      }
+      continue;
+    }
+    // two ACS steps (kinds 1 and 2: layout 0 again after them); a lane the first
+    // step sends back to a walk waits out the second
+    if (__ballot(mode == kWalkPend) != 0u) unpack(IntC<0>{});
+    acs_step(IntC<1>{});
+    acs_step(IntC<2>{});
+  }
+  if (valid && a.sums) {
+    const int64_t qe = qwave + lane_id();
+    a.sums[2 * qe] = lp;
+    a.sums[2 * qe + 1] = lr;
+  }
+  count_decisions_masked(vmask, vmask, lp, lr, a.counts);
+}
+
 template <int m, bool kSpec, uint64_t XM, bool kTrace>
 __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
   constexpr int M = 1 << m, H = M / 2, NW = M / 8, R = 4;
@@ -636,10 +850,24 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
   // Sequence index without a VGPR live across the step loop: the wave's first
   // index in SGPRs, the lane from mbcnt, recomputed after the loop; validity
   // and hypothesis as wave ballots (SGPRs)
-  const int64_t qwave = (int64_t)blockIdx.x * kBlock + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  int64_t gw = (int64_t)blockIdx.x * (kBlock / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
+  if (!kTrace && a.walk) {
+    // H1 and H2 waves alternate (the pair order flips with the block), so every SIMD
+    // holds both: the walks' load latency hides under the H2 waves' ACS
+    // (waves past 2 * half are the grid's padding and stay past the sequences)
+    const int64_t half = ((a.nseq + 63) / 64 + 1) / 2, k = gw >> 1;
+    if (gw < 2 * half) gw = ((gw ^ (gw >> 2)) & 1) ? half + k : k;
+  }
+  const int64_t qwave = gw * 64;
   const int64_t q = qwave + lane_id();
   const bool valid = q < a.nseq;
   const uint64_t vmask = __ballot(valid), hmask = __ballot(q < a.n_h1);
+  if constexpr (kSpec && !kTrace) {
+    if (a.walk && vmask != 0u && hmask == vmask) {
+      k1b_walk<m, XM>(a, qwave, vmask, s_lt);
+      return;
+    }
+  }
   double lp = 0.0, lr = 0.0;
   if (valid) {
     // Pairs (D(2i), D(2i+1)), packed 16-bit.  Table-driven kernel: D + O, O the

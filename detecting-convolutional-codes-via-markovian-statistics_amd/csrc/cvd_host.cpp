@@ -559,16 +559,29 @@ void build_hash(cvd_model& Mo) {
     for (int w = 0; w < nw; ++w) Mo.h_key[slot * ssw + w] = kw[w];
     slot_of[(size_t)i] = (int64_t)slot;
   }
+  // row keys by device row id (the walk mode of the specialised kernel rebuilds a
+  // lane's metric vector from the key of the last row it walked)
+  Mo.h_dkey.assign((size_t)Mo.n_rows * nw, 0u);
+  const Tabs T = make_tabs(Mo.dec);
   parallel_for(Mo.n_rows, [&](int64_t i, int) {
-    // entry r = 16 bytes {log P̂1[r] (f64), successor row (i32, -1: none), 0}: one
-    // 12-byte device load per step
+    // entry r = 16 bytes {log P̂1[r] (f64), successor row (i32, -1: none), T_ref count
+    // c(r)}: one 12-byte device load per step (16 in walk mode).  c(r) = the words q
+    // with successor(q) == successor(r) as metric vectors (Pd_plotter.py:89-99, the
+    // |Y| the butterfly kernel derives from the halves test).
     uint32_t* dw = Mo.h_drow.data() + (size_t)dev_of[(size_t)i] * Mo.h_rsw;
+    const uint8_t* D = Mo.keys.data() + (size_t)i * M;
+    uint8_t succ[16][256];
+    for (int r = 0; r < R; ++r) step_host(T, D, (uint32_t)r, succ[r]);
     for (int r = 0; r < R; ++r) {
       std::memcpy(dw + 4 * r, Mo.logp1.data() + (size_t)i * R + r, sizeof(double));
       const int64_t j = Mo.row_next[(size_t)i * R + r];
       dw[4 * r + 2] = (uint32_t)(j >= 0 ? (int32_t)dev_of[(size_t)j] : -1);
-      dw[4 * r + 3] = 0u;
+      uint32_t c = 0u;
+      for (int q2 = 0; q2 < R; ++q2) c += std::memcmp(succ[q2], succ[r], (size_t)M) == 0;
+      dw[4 * r + 3] = c;
     }
+    std::memcpy(Mo.h_dkey.data() + (size_t)dev_of[(size_t)i] * nw, kws.data() + (size_t)i * nw,
+                sizeof(uint32_t) * (size_t)nw);
     uint32_t* hw = interleave ? Mo.h_key.data() + (size_t)slot_of[(size_t)i] * ssw + nw
                               : Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw;
     std::memcpy(hw, dw, sizeof(uint32_t) * Mo.h_rsw);

@@ -40,7 +40,9 @@ struct cvd_model {
   int32_t h_rsw = 0;              // row record stride in dwords (row_words)
   int32_t h_ssw = 0;              // directory slot stride in dwords: nw, or (CVD_SLOT_IL) key + record in one slot
   std::vector<uint32_t> h_row;    // [hcap][h_rsw]: per r, 16 B {log P̂1[r] (f64), successor row[r] (i32, -1: none), 0}
-  std::vector<uint32_t> h_drow;   // [n_rows][h_rsw]: the same records dense by row id (table mode)
+  std::vector<uint32_t> h_drow;   // [n_rows][h_rsw]: the same records dense by row id (table mode),
+                                  // dword 3 of entry r = the T_ref count c(r)
+  std::vector<uint32_t> h_dkey;   // [n_rows][NW]: row keys (device layout) by device row id
   int32_t slot0 = 0;              // row of D_0 = 0 (always 0)
   std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
   // k = 1 orbit kernel: successor(r ^ g0) = successor(r) with states 2j <-> 2j+1 swapped,
@@ -67,6 +69,7 @@ struct cvd_model {
   uint32_t* d_hkey = nullptr;
   uint32_t* d_hrow = nullptr;
   uint32_t* d_drow = nullptr;
+  uint32_t* d_dkey = nullptr;
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
   uint32_t* d_bfly = nullptr;

@@ -1401,6 +1401,25 @@ int cvd::explicit_kernel_of(const cvd_model& M) {
   return select_explicit(M, kExplicitBest, &k, &b);
 }
 
+static int env_i(const char* name, int def) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atoi(e) : def;
+}
+
+// k1b_walk (cvd_device.h) for the H1 waves of the specialised kernel.  Its walks pay
+// only when nearly every H1 step stays in learned rows: the learning chain is the H1
+// streams' own process, so rows / learn_len estimates the share of steps that leave
+// them (m = 6, learn_len 10^6: 0.030 at p = 0.01, where H1 rows hold D_t 98% of the
+// time and the launch takes 526 instead of 621 ms; 0.070 at p = 0.02: 636 vs 635;
+// 0.32 at p = 0.05: 1,127 vs 681 -- a lane that leaves its walk waits for an ACS step
+// of its wave, and those run with few lanes; profiles/r03i_walk/).  CVD_WALK=0 / 1
+// forces it off / on (timing studies; the sums are the same).
+static bool walk_preferred(const cvd_model& M) {
+  const int e = env_i("CVD_WALK", -1);
+  if (e >= 0) return e != 0;
+  return M.kind == 1 && M.learn_len_eff > 0 && 25 * M.n_rows < M.learn_len_eff;
+}
+
 int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                                 int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
                                 void* stream, int variant, bool early) {
@@ -1426,6 +1445,14 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   a.trace = d_trace;
   a.early = early && !d_sums && !d_trace; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
+  a.dkey = M.d_dkey;
+  a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !a.early && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey &&
+           walk_preferred(M);
+  // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
+  // lanes), or while < 8 lanes wait for the ACS (profiles/r03i_walk/ab_policy.jsonl)
+  a.walk_wmin = env_i("CVD_WALK_WMIN", 48);
+  a.walk_amin = env_i("CVD_WALK_AMIN", 8);
+  a.walk_burst = std::max(1, std::min(16, env_i("CVD_WALK_BURST", 16)));   // <= 16 (k1b_walk's word buffer)
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
   if (which == CVD_KERNEL_BUTTERFLY_RTC) {
     void* args[] = {&a};
@@ -1460,6 +1487,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_hkey, M.h_key))) return rc;
     if ((rc = dev_copy(M.d_hrow, M.h_row))) return rc;
     if ((rc = dev_copy(M.d_drow, M.h_drow))) return rc;
+    if ((rc = dev_copy(M.d_dkey, M.h_dkey))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
     if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
     if ((rc = dev_copy(M.d_bfly, M.bfly))) return rc;
@@ -1486,11 +1514,13 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_hkey, M.d_hrow, M.d_drow, M.d_bmp, M.d_bmk1, M.d_bfly};
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_bmp, M.d_bmk1,
+                  M.d_bfly};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
-  M.d_filt = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_bmp = nullptr; M.d_bmk1 = nullptr;
+  M.d_filt = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_bmp = nullptr;
+  M.d_bmk1 = nullptr;
   M.d_bfly = nullptr;
   M.rtc_fn = nullptr;
   M.device = -1;

@@ -10,7 +10,8 @@ rounds x variants detector launches are timed with HIP events on the launch
 stream, and every variant's per-trial sums must equal the first variant's.
 
 usage: python profiles/ab_k1b.py --variant= --variant=-DCVD_K1B_WAVES=5 --p 0.01 0.1
-       (host-side settings after a ';': --variant=";CVD_FILTER_SCALE=-1")
+       (host-side settings after a ';': --variant=";CVD_FILTER_SCALE=-1"; they are set at model
+       build and around every launch of the variant, e.g. --variant=";CVD_WALK=0")
 prints one JSON line per p: per-variant launch times (ms), medians and mins.
 """
 import argparse
@@ -53,9 +54,11 @@ def main():
         det.generate(g1, N, p, a.seed, tag, 0, 2, B, out=r, q0=0, pitch=2 * B)
         det.generate(g2, N, p, a.seed, tag, 1, 2, B, out=r, q0=B, pitch=2 * B)
         models = []
+        envs_of = {}
         for v in a.variants:
             # a variant is JIT defines, optionally followed by ";VAR=value" host settings
             defs, *envs = v.split(";")
+            envs_of[v] = [e.split("=", 1) for e in envs]
             os.environ["CVD_JIT_DEFINES"] = defs
             for e in envs:
                 k_, v_ = e.split("=", 1)
@@ -65,10 +68,19 @@ def main():
                 os.environ.pop(e.split("=", 1)[0], None)
         os.environ.pop("CVD_JIT_DEFINES", None)
         kernels = [pkg.KERNEL_NAMES[mod.info()["explicit_kernel"]] for mod in models]
+        def launch_env(v, on):
+            for k_, v_ in envs_of[v]:
+                if on:
+                    os.environ[k_] = v_
+                else:
+                    os.environ.pop(k_, None)
+
         ref = None
         for v, mod in zip(a.variants, models):   # correctness: identical sums for every variant
             sums = torch.empty((2 * B, 2), dtype=torch.float64, device=det.device)
+            launch_env(v, True)
             det.detect(mod, r, N, 2 * B, B, sums=sums)
+            launch_env(v, False)
             s = sums.cpu().numpy()
             if ref is None:
                 ref = s
@@ -80,9 +92,11 @@ def main():
         for _ in range(a.rounds):
             for v, mod in zip(a.variants, models):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                launch_env(v, True)
                 e0.record(stream)
                 det.detect(mod, r, N, 2 * B, B, counts=counts, stream=stream)
                 e1.record(stream)
+                launch_env(v, False)
                 e1.synchronize()
                 times[v].append(e0.elapsed_time(e1))
         line = {"p": p, "trials": B, "N": N, "kernels": kernels, "ms": times,

@@ -1,0 +1,68 @@
+"""Walk mode of the specialised m = 6 kernel (cvd_device.h k1b_walk): H1 lanes that sit
+in learned rows take their steps from the row records (log P̂1, successor, T_ref count
+c) without the ACS, and rebuild the metric vector from the row key when they leave.
+Per-trial fp64 sums and counts must equal the lockstep kernel's (CVD_WALK=0) bit for
+bit -- and the C oracle's -- at every p of the sweep, for trial counts that are not
+whole waves (one wave mixes H1 and H2 lanes), N not a multiple of the 16-step word,
+and every schedule extreme (burst of one step, always / never preferring walks)."""
+import numpy as np
+import pytest
+
+from oracle import c_oracle as C
+
+pytestmark = pytest.mark.gpu
+
+SEED = 12345
+
+
+def _m6(pkg):
+    cc = pkg.CONFIG_CODES["m6"]
+    return cc, pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+
+
+def _sums(det, model, cc, N, p, t0, t1):
+    s = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, SEED, t0, t1, return_sums=True)
+    return s["sums"], s["counts"].cpu().tolist()
+
+
+@pytest.mark.parametrize("p", [0.01, 0.02, 0.05, 0.1, 0.2])
+def test_walk_equals_lockstep(pkg, monkeypatch, p):
+    cc, det = _m6(pkg)
+    model = det.model(p, 200_000, 200, 1.0, SEED)
+    for N, t0, t1 in [(1237, 0, 300), (4096, 1_000_003, 1_000_003 + 128)]:
+        monkeypatch.setenv("CVD_WALK", "0")
+        ref, rc = _sums(det, model, cc, N, p, t0, t1)
+        monkeypatch.setenv("CVD_WALK", "1")
+        got, gc = _sums(det, model, cc, N, p, t0, t1)
+        assert np.array_equal(got, ref), (p, N)
+        assert gc == rc
+
+
+@pytest.mark.parametrize("wmin,amin,burst", [("1", "64", "1"), ("64", "1", "3"), ("8", "16", "64")])
+def test_walk_schedules(pkg, monkeypatch, wmin, amin, burst):
+    """Schedule knobs change only the order of work, never a sum."""
+    cc, det = _m6(pkg)
+    p = 0.03
+    model = det.model(p, 200_000, 200, 1.0, SEED)
+    monkeypatch.setenv("CVD_WALK", "0")
+    ref, rc = _sums(det, model, cc, 3000, p, 0, 200)
+    monkeypatch.setenv("CVD_WALK", "1")
+    monkeypatch.setenv("CVD_WALK_WMIN", wmin)
+    monkeypatch.setenv("CVD_WALK_AMIN", amin)
+    monkeypatch.setenv("CVD_WALK_BURST", burst)
+    got, gc = _sums(det, model, cc, 3000, p, 0, 200)
+    assert np.array_equal(got, ref)
+    assert gc == rc
+
+
+def test_walk_equals_c_oracle(pkg, monkeypatch):
+    cc, det = _m6(pkg)
+    p, N, T = 0.02, 5000, 192
+    monkeypatch.setenv("CVD_WALK", "1")
+    model = det.model(p, 300_000, 200, 1.0, SEED)
+    got, gc = _sums(det, model, cc, N, p, 0, T)
+    c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
+    cnt, sums = C.Model(c1, p, 300_000, 200, 1.0, SEED).run_trials(c1, c2, N, p, SEED, 0, T, sums=True,
+                                                                    nthreads=8)
+    assert np.array_equal(got, sums)
+    assert gc == [int(x) for x in cnt]
