@@ -668,10 +668,16 @@ struct IntC {
 // mu_prev = 0 (pairs = D + 1).  Per-trial sums are the lockstep body's bit for bit:
 // each lane adds the same terms in step order.
 enum : uint32_t { kWalkAcs = 0u, kWalkPend = 1u, kWalkWalk = 2u, kWalkDone = 3u };
+// timing ablation (CVD_JIT_DEFINES=-DCVD_WALK_ABL=1, results differ): walk-mode waves
+// do no work, so the launch times the H2 waves alone
+#ifndef CVD_WALK_ABL
+#define CVD_WALK_ABL 0
+#endif
 
 template <int m, uint64_t XM>
 __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64_t vmask, const double* s_lt) {
   constexpr int M = 1 << m, H = M / 2, NW = M / 8, R = 4;
+  if (CVD_WALK_ABL & 1) return;
   const bool valid = qwave + lane_id() < a.nseq;
   const uint32_t N = (uint32_t)a.N;
   const uint32_t nwords = (N + 15u) / 16u;
