@@ -1,6 +1,11 @@
+/* Share of steps whose D_t is a learned row, along H1 / H2 sequences of the m = 6 bench
+ * models (learn_len 10^6), from the C oracle's own model and streams (measurement tool,
+ * not product code): rowfrac, out-of-row segments per 1000 steps and their mean length,
+ * the share of wave-steps where all 64 H1 lanes sit in rows, and a log2 histogram of the
+ * out-of-row segment lengths.  DESIGN.md "Walk mode" quotes it.
+ *   gcc -O2 -fopenmp -I../../oracle -o row_share row_share.c -lm && ./row_share 20000 2 */
 #include <stdio.h>
-#include "/root/repo/oracle/cvd_oracle.c"
-/* segment statistics of D_t row membership along H1/H2 sequences (m6 bench models) */
+#include "cvd_oracle.c"
 int main(int argc, char** argv) {
   const double ps[6] = {0.01, 0.02, 0.05, 0.1, 0.15, 0.2};
   static const uint8_t t1[] = {1,0,1,1,0,1,1, 1,1,1,1,0,0,1};
