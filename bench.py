@@ -431,6 +431,8 @@ def main():
                        "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
                        "detector_ms_steps": det_each,
                        "generator_pmc": gen_pmc,
+                       # walk mode of the m = 6 kernel per grid point (cvd_model_info.walk)
+                       "walk_by_p": {str(p): int(models[p].info().get("walk", 0)) for p in p_grid} if models else None,
                        "per_p": per_p},
     }
     if early_out is not None:

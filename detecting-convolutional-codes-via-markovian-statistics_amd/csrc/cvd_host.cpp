@@ -1058,6 +1058,7 @@ extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
   info->logp1_unseen = Mo->logp1_unseen;
   info->explicit_kernel = explicit_kernel_of(*Mo);
   info->mc_fused = mc_fused_preferred(*Mo) ? 1 : 0;
+  info->walk = Mo->k1b_ok && Mo->hcap > 0 && walk_preferred(*Mo) ? 1 : 0;
   return CVD_OK;
 }
 

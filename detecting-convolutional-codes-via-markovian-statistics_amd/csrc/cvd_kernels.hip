@@ -1414,7 +1414,7 @@ static int env_i(const char* name, int def) {
 // 0.32 at p = 0.05: 1,127 vs 681 -- a lane that leaves its walk waits for an ACS step
 // of its wave, and those run with few lanes; profiles/r03i_walk/).  CVD_WALK=0 / 1
 // forces it off / on (timing studies; the sums are the same).
-static bool walk_preferred(const cvd_model& M) {
+bool cvd::walk_preferred(const cvd_model& M) {
   const int e = env_i("CVD_WALK", -1);
   if (e >= 0) return e != 0;
   return M.kind == 1 && M.learn_len_eff > 0 && 25 * M.n_rows < M.learn_len_eff;

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 5
+#define CVD_ABI_VERSION 6
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -85,6 +85,10 @@ typedef struct cvd_model_info {
                               (cvd_mc_fused) for this model: an LDS-resident table small enough for
                               256-thread blocks (measured faster there; the 1024-thread variant of the
                               large tables is slower than the two-kernel pipeline) */
+  int32_t walk;            /* 1: the specialised m = 6 kernel runs this model's H1 waves in walk mode
+                              (learned-row steps from the row records, no ACS; sums unchanged): the
+                              model's rows / learn_len < 1/25, i.e. H1 stays in learned rows (CVD_WALK
+                              overrides; counts-only early decision and traces always run lockstep) */
 } cvd_model_info;
 
 #define CVD_KERNEL_NONE 0       /* explicit path unsupported for this shape */

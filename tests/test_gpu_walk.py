@@ -66,3 +66,20 @@ def test_walk_equals_c_oracle(pkg, monkeypatch):
                                                                     nthreads=8)
     assert np.array_equal(got, sums)
     assert gc == [int(x) for x in cnt]
+
+
+def test_walk_flag_follows_row_share(pkg, monkeypatch):
+    """cvd_model_info.walk: on where the model's rows / learn_len < 1/25 (H1 stays in rows),
+    off elsewhere and for dense models; CVD_WALK forces it."""
+    cc, det = _m6(pkg)
+    monkeypatch.delenv("CVD_WALK", raising=False)
+    lo = det.model(0.01, 1_000_000, 200, 1.0, SEED).info()
+    hi = det.model(0.1, 1_000_000, 200, 1.0, SEED).info()
+    assert 25 * lo["n_rows"] < lo["learn_len_eff"] and lo["walk"] == 1
+    assert 25 * hi["n_rows"] >= hi["learn_len_eff"] and hi["walk"] == 0
+    monkeypatch.setenv("CVD_WALK", "1")
+    assert det.model(0.1, 1_000_000, 200, 1.0, SEED).info()["walk"] == 1
+    m2 = pkg.CONFIG_CODES["m2"]
+    d2 = pkg.Detector(1, 2, 2, m2["gen1"], device=0)
+    monkeypatch.delenv("CVD_WALK")
+    assert d2.model(0.05, None, 200, 1.0, SEED).info()["walk"] == 0
