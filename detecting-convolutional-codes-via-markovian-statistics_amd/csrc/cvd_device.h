@@ -793,6 +793,7 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
   const int burst = a.walk_burst;
   // every iteration moves a lane a step or out of a walk: 2 (N + 1) per lane bound it
   // (a guard only: the loop ends by itself)
+  int64_t st_acs = 0, st_burst = 0, st_biter = 0, st_unpack = 0, st_lanes_acs = 0, st_lanes_walk = 0;
   for (int64_t it = 0, it_max = 128 * ((int64_t)N + 1); it < it_max; ++it) {
     if (need) {
       nxtw = load_word((pos >> 4) + 1u);
@@ -802,7 +803,9 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
     if ((mA | mW) == 0u) break;
     const uint32_t nA = (uint32_t)__popcll(mA), nW = (uint32_t)__popcll(mW);
     if (nW != 0u && (nA == 0u || nW >= wmin || nA < amin)) {
+      if (CVD_WALK_ABL & 2) { ++st_burst; st_lanes_walk += nW; }
       for (int b = 0; b < burst; ++b) {
+        if (CVD_WALK_ABL & 2) ++st_biter;
         if (mode == kWalkWalk) {
           if (cur.pnx < 0) {
             // D_t is not a row: rebuild D_{t-1} (row `slot`) for the ACS
@@ -832,10 +835,19 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
     }
     // two ACS steps (kinds 1 and 2: layout 0 again after them); a lane the first
     // step sends back to a walk waits out the second
-    if (__ballot(mode == kWalkPend) != 0u) unpack(IntC<0>{});
+    if (__ballot(mode == kWalkPend) != 0u) {
+      if (CVD_WALK_ABL & 2) ++st_unpack;
+      unpack(IntC<0>{});
+    }
+    if (CVD_WALK_ABL & 2) { ++st_acs; st_lanes_acs += nA; }
     acs_step(IntC<1>{});
     acs_step(IntC<2>{});
   }
+  // (CVD_WALK_ABL & 2: schedule statistics of the first H1 waves, printed; sums unchanged)
+  if ((CVD_WALK_ABL & 2) && qwave < 4 * 64 * 4 && lane_id() == 0)
+    printf("walkstats q0=%lld acs_pairs=%lld lanes_per_acs=%.1f bursts=%lld burst_iters=%lld walkers_per_burst=%.1f unpacks=%lld\n",
+           (long long)qwave, (long long)st_acs, st_acs ? (double)st_lanes_acs / st_acs : 0.0, (long long)st_burst,
+           (long long)st_biter, st_burst ? (double)st_lanes_walk / st_burst : 0.0, (long long)st_unpack);
   if (valid && a.sums) {
     const int64_t qe = qwave + lane_id();
     a.sums[2 * qe] = lp;
