@@ -714,6 +714,13 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
   cur.slot = -1; cur.pnx = -1; cur.hs = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u;
   cur.cand = false; cur.plp = 0.0; cur.pc = 1u;
   uint32_t mode = kWalkDone;
+  int dec = 0;   // early decision of this lane (counts only): checked every kEarlyEvery of its steps
+  // after a step: the lane is done at N, or (early decision) once its decision is certain
+  auto finished = [&]() -> bool {
+    if (pos == N) return true;
+    if (a.early && (pos & (uint32_t)(kEarlyEvery - 1)) == 0u) dec = early_decide(lp, lr, (int64_t)(N - pos), a.lt_min, a.lp_min);
+    return dec != 0;
+  };
   if (valid && N > 0u) {
     curw = load_word(0u);
     nxtw = load_word(1u);
@@ -780,7 +787,7 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
       kmu8 = off8;
       mu_prev = mu;
       advance();
-      if (pos == N) {
+      if (finished()) {
         mode = kWalkDone;
         cur.slot = -1;
       } else {
@@ -821,7 +828,7 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
             lr += s_lt[cur.pc];
             cur.slot = cur.pnx;
             advance();
-            if (pos == N) {
+            if (finished()) {
               mode = kWalkDone;
               cur.slot = -1;
             } else {
@@ -853,6 +860,7 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
     a.sums[2 * qe] = lp;
     a.sums[2 * qe + 1] = lr;
   }
+  early_final(dec, lp, lr);
   count_decisions_masked(vmask, vmask, lp, lr, a.counts);
 }
 

@@ -98,7 +98,7 @@ int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int6
 // pipeline (small LDS tables: 256-thread blocks); cvd_mc_run's AUTO path uses it then
 bool mc_fused_preferred(const cvd_model& M);
 // the specialised butterfly kernel runs the model's H1 waves in walk mode (k1b_walk)
-bool walk_preferred(const cvd_model& M);
+bool walk_preferred(const cvd_model& M, bool early = false);
 int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
                     uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,
                     int64_t* d_counts, void* stream, bool early);

@@ -1413,11 +1413,13 @@ static int env_i(const char* name, int def) {
 // time and the launch takes 526 instead of 621 ms; 0.070 at p = 0.02: 636 vs 635;
 // 0.32 at p = 0.05: 1,127 vs 681 -- a lane that leaves its walk waits for an ACS step
 // of its wave, and those run with few lanes; profiles/r03i_walk/).  CVD_WALK=0 / 1
-// forces it off / on (timing studies; the sums are the same).
-bool cvd::walk_preferred(const cvd_model& M) {
+// forces it off / on (timing studies; the sums are the same).  Counts-only early decision
+// stays lockstep unless forced: there walk mode measured slower (p = 0.01: 700 vs 648 ms
+// per 2,621,440-trial launch, profiles/r03i_walk/bench_early_walk.json).
+bool cvd::walk_preferred(const cvd_model& M, bool early) {
   const int e = env_i("CVD_WALK", -1);
   if (e >= 0) return e != 0;
-  return M.kind == 1 && M.learn_len_eff > 0 && 25 * M.n_rows < M.learn_len_eff;
+  return !early && M.kind == 1 && M.learn_len_eff > 0 && 25 * M.n_rows < M.learn_len_eff;
 }
 
 int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
@@ -1446,8 +1448,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   a.trace = d_trace;
   a.early = early && !d_sums && !d_trace; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
   a.dkey = M.d_dkey;
-  a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !a.early && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey &&
-           walk_preferred(M);
+  a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
   // lanes), or while < 8 lanes wait for the ACS (profiles/r03i_walk/ab_policy.jsonl)
   a.walk_wmin = env_i("CVD_WALK_WMIN", 48);

@@ -88,7 +88,8 @@ typedef struct cvd_model_info {
   int32_t walk;            /* 1: the specialised m = 6 kernel runs this model's H1 waves in walk mode
                               (learned-row steps from the row records, no ACS; sums unchanged): the
                               model's rows / learn_len < 1/25, i.e. H1 stays in learned rows (CVD_WALK
-                              overrides; counts-only early decision and traces always run lockstep) */
+                              overrides; traces and, unless CVD_WALK=1, counts-only early decision
+                              run lockstep) */
 } cvd_model_info;
 
 #define CVD_KERNEL_NONE 0       /* explicit path unsupported for this shape */

@@ -68,6 +68,22 @@ def test_walk_equals_c_oracle(pkg, monkeypatch):
     assert gc == [int(x) for x in cnt]
 
 
+@pytest.mark.parametrize("p", [0.01, 0.05])
+def test_walk_early_decision_counts(pkg, monkeypatch, p):
+    """Early decision in walk mode (each lane stops once certain, checked every 128 of its
+    own steps): the full run's counts."""
+    cc, det = _m6(pkg)
+    model = det.model(p, 200_000, 200, 1.0, SEED)
+    monkeypatch.setenv("CVD_WALK", "1")
+    full = det.run_trials(model, cc["gen1"], cc["gen2"], 20_000, p, SEED, 0, 640)["counts"].cpu().tolist()
+    early = det.run_trials(model, cc["gen1"], cc["gen2"], 20_000, p, SEED, 0, 640,
+                           early_decision=True)["counts"].cpu().tolist()
+    monkeypatch.setenv("CVD_WALK", "0")
+    lock = det.run_trials(model, cc["gen1"], cc["gen2"], 20_000, p, SEED, 0, 640,
+                          early_decision=True)["counts"].cpu().tolist()
+    assert early == full == lock
+
+
 def test_walk_flag_follows_row_share(pkg, monkeypatch):
     """cvd_model_info.walk: on where the model's rows / learn_len < 1/25 (H1 stays in rows),
     off elsewhere and for dense models; CVD_WALK forces it."""
