@@ -139,6 +139,7 @@ struct ExpArgs {
   const uint32_t* drow;     // [rows][row_words(n)]: the same records dense by row id (table mode)
   const uint32_t* dkey;     // [rows][NW]: the key of every learned row by row id (k1b_walk: a lane leaving
                             // a table walk rebuilds its metric vector from it)
+  const uint32_t* t2;       // [rows][16][8] two-step walk records (k1b_walk; null: one step per load)
   const double* ltref;      // [R + 1]
   const uint32_t* bmp;      // branch-metric table (kernel-specific layout)
   uint32_t repmap, swmap;   // k = 1 orbit kernel: rep index / swap flag per received word
@@ -385,12 +386,12 @@ struct RowCursor {
   // D_t's key is known: issue the next step's loads
   // kmu8: the key's offset c * 0x11111111, c in {kLo, kLo + 1}
   // hi: the offset is kLo + 1 (else kLo), as a flag the caller already has
-  template <int kLo = 0, bool kC = false>
+  template <int kLo = 0, bool kC = false, bool kRow = true>
   __device__ void prefetch(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t rn, uint32_t kmu8 = 0u,
                            bool hi = false) {
     if (CVD_ABL & 1) return;
     if (slot >= 0) {
-      prefetch_row<kC>(a, slot, rn);
+      if (kRow) prefetch_row<kC>(a, slot, rn);
     } else if (slot == -2 && !(CVD_ABL & 4)) {
       uint32_t ph, pl;
       cvd::key_hash_less<kLo>(key_in, NW, kLo + (hi ? 1u : 0u), ph, pl);   // = key_hash(key_in - kmu8)
@@ -713,6 +714,25 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
   RowCursor<NW, R> cur;
   cur.slot = -1; cur.pnx = -1; cur.hs = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u;
   cur.cand = false; cur.plp = 0.0; cur.pc = 1u;
+  // the entry a walker consumes next: one step (cur.plp / pnx / pc, a drow entry) or, with
+  // two-step records and two steps left, {cur.plp, plp2, cur.pnx, cur.pc} = the t2 record
+  // {log P̂1 of both steps, (d1 + 1) | c1 << 28, (d2 + 1) | c2 << 28}
+  double plp2 = 0.0;
+  auto two_steps = [&]() -> bool { return a.t2 != nullptr && pos + 2u <= N; };
+  auto walk_prefetch = [&]() {
+    const uint32_t x = __builtin_amdgcn_alignbit(nxtw, curw, 2u * (pos & 15u));   // r of steps pos + 1, pos + 2
+    if (two_steps()) {
+      const uint32_t* e = a.t2 + ((size_t)cur.slot * 16u + (x & 15u)) * 8u;
+      const uint4 v = *reinterpret_cast<const uint4*>(e);
+      const uint2 w = *reinterpret_cast<const uint2*>(e + 4);
+      cur.pc = w.y;
+      cur.pnx = (int32_t)w.x;
+      plp2 = __hiloint2double((int)v.w, (int)v.z);
+      cur.plp = __hiloint2double((int)v.y, (int)v.x);
+    } else {
+      cur.template prefetch_row<true>(a, cur.slot, x & 3u);
+    }
+  };
   uint32_t mode = kWalkDone;
   int dec = 0;   // early decision of this lane (counts only): checked every kEarlyEvery of its steps
   // after a step: the lane is done at N, or (early decision) once its decision is certain
@@ -725,7 +745,7 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
     curw = load_word(0u);
     nxtw = load_word(1u);
     cur.slot = a.slot0;   // D_0 = 0 is a learned row: every lane starts walking
-    cur.template prefetch_row<true>(a, cur.slot, curw & 3u);
+    walk_prefetch();
     mode = kWalkWalk;
   }
   // Before an ACS step with PEND lanes: every lane's pairs from a canonical key (no
@@ -791,8 +811,11 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
         mode = kWalkDone;
         cur.slot = -1;
       } else {
-        cur.template prefetch<1, true>(a, key, word_at() & 3u, kmu8, mu != 0u);
-        if (cur.slot >= 0) mode = kWalkWalk;
+        cur.template prefetch<1, true, false>(a, key, word_at() & 3u, kmu8, mu != 0u);   // hashed lookups
+        if (cur.slot >= 0) {
+          mode = kWalkWalk;
+          walk_prefetch();
+        }
       }
     }
   };
@@ -814,26 +837,57 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
       for (int b = 0; b < burst; ++b) {
         if (CVD_WALK_ABL & 2) ++st_biter;
         if (mode == kWalkWalk) {
-          if (cur.pnx < 0) {
-            // D_t is not a row: rebuild D_{t-1} (row `slot`) for the ACS
+          // D_t is not a row: rebuild D_{t-1} (row `slot`) for the ACS; the ACS step takes
+          // log P̂1 from cur.plp with successor -1
+          auto leave = [&]() {
             mode = kWalkPend;
+            cur.pnx = -1;
             const uint32_t* kp = a.dkey + (size_t)cur.slot * NW;
 #pragma unroll
             for (int i = 0; i < NW / 4; ++i) {
               const uint4 v = *reinterpret_cast<const uint4*>(kp + 4 * i);
               Dp[4 * i] = v.x; Dp[4 * i + 1] = v.y; Dp[4 * i + 2] = v.z; Dp[4 * i + 3] = v.w;
             }
+          };
+          auto done = [&]() {
+            mode = kWalkDone;
+            cur.slot = -1;
+          };
+          if (two_steps()) {
+            const int32_t d1 = (int32_t)((uint32_t)cur.pnx & 0x0FFFFFFFu) - 1;
+            if (d1 < 0) {
+              leave();
+            } else {
+              lp += cur.plp;                 // Pd_plotter.py:115, from the row's records
+              lr += s_lt[(uint32_t)cur.pnx >> 28];
+              cur.slot = d1;
+              advance();
+              if (finished()) {
+                done();
+              } else {
+                const int32_t d2 = (int32_t)(cur.pc & 0x0FFFFFFFu) - 1;
+                if (d2 < 0) {
+                  cur.plp = plp2;
+                  leave();
+                } else {
+                  lp += plp2;
+                  lr += s_lt[cur.pc >> 28];
+                  cur.slot = d2;
+                  advance();
+                  if (finished()) done();
+                  else walk_prefetch();
+                }
+              }
+            }
+          } else if (cur.pnx < 0) {
+            leave();
           } else {
             lp += cur.plp;                   // Pd_plotter.py:115, from the row's record
             lr += s_lt[cur.pc];
             cur.slot = cur.pnx;
             advance();
-            if (finished()) {
-              mode = kWalkDone;
-              cur.slot = -1;
-            } else {
-              cur.template prefetch_row<true>(a, cur.slot, word_at() & 3u);
-            }
+            if (finished()) done();
+            else walk_prefetch();
           }
         }
         if (__ballot(mode == kWalkWalk) == 0u) break;

@@ -587,6 +587,31 @@ void build_hash(cvd_model& Mo) {
     std::memcpy(hw, dw, sizeof(uint32_t) * Mo.h_rsw);
   });
   Mo.slot0 = (int32_t)dev_of[0];   // D_0 = 0 is row 0 in both model kinds
+  // two-step walk records (k1b_walk), for models that walk: per device row d and word pair
+  // (r1, r2), 32 B {log P̂1(d, r1), log P̂1(d1, r2), (d1 + 1) | c(d, r1) << 28,
+  // (d2 + 1) | c(d1, r2) << 28}, d1 / d2 the rows after one / two steps (0 = not a row)
+  Mo.h_t2.clear();
+  if (Mo.dec.k == 1 && R == 4 && walk_preferred(Mo)) {
+    Mo.h_t2.assign((size_t)Mo.n_rows * 16 * 8, 0u);
+    parallel_for(Mo.n_rows, [&](int64_t d, int) {
+      const uint32_t* a0 = Mo.h_drow.data() + (size_t)d * Mo.h_rsw;
+      for (int r1 = 0; r1 < 4; ++r1) {
+        const int32_t d1 = (int32_t)a0[4 * r1 + 2];
+        for (int r2 = 0; r2 < 4; ++r2) {
+          uint32_t* e = Mo.h_t2.data() + ((size_t)d * 16 + (size_t)(r1 | (r2 << 2))) * 8;
+          e[0] = a0[4 * r1];
+          e[1] = a0[4 * r1 + 1];
+          e[4] = (uint32_t)(d1 + 1) | (a0[4 * r1 + 3] << 28);
+          if (d1 >= 0) {
+            const uint32_t* a1 = Mo.h_drow.data() + (size_t)d1 * Mo.h_rsw;
+            e[2] = a1[4 * r2];
+            e[3] = a1[4 * r2 + 1];
+            e[5] = (uint32_t)((int32_t)a1[4 * r2 + 2] + 1) | (a1[4 * r2 + 3] << 28);
+          }
+        }
+      }
+    });
+  }
 }
 
 void build_bmk1(cvd_model& Mo, const Tabs& T) {

@@ -43,6 +43,7 @@ struct cvd_model {
   std::vector<uint32_t> h_drow;   // [n_rows][h_rsw]: the same records dense by row id (table mode),
                                   // dword 3 of entry r = the T_ref count c(r)
   std::vector<uint32_t> h_dkey;   // [n_rows][NW]: row keys (device layout) by device row id
+  std::vector<uint32_t> h_t2;     // [n_rows][16][8]: two-step walk records (walking models only)
   int32_t slot0 = 0;              // row of D_0 = 0 (always 0)
   std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
   // k = 1 orbit kernel: successor(r ^ g0) = successor(r) with states 2j <-> 2j+1 swapped,
@@ -70,6 +71,7 @@ struct cvd_model {
   uint32_t* d_hrow = nullptr;
   uint32_t* d_drow = nullptr;
   uint32_t* d_dkey = nullptr;
+  uint32_t* d_t2 = nullptr;
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
   uint32_t* d_bfly = nullptr;

@@ -1409,17 +1409,17 @@ static int env_i(const char* name, int def) {
 // k1b_walk (cvd_device.h) for the H1 waves of the specialised kernel.  Its walks pay
 // only when nearly every H1 step stays in learned rows: the learning chain is the H1
 // streams' own process, so rows / learn_len estimates the share of steps that leave
-// them (m = 6, learn_len 10^6: 0.030 at p = 0.01, where H1 rows hold D_t 98% of the
-// time and the launch takes 526 instead of 621 ms; 0.070 at p = 0.02: 636 vs 635;
-// 0.32 at p = 0.05: 1,127 vs 681 -- a lane that leaves its walk waits for an ACS step
-// of its wave, and those run with few lanes; profiles/r03i_walk/).  CVD_WALK=0 / 1
+// them (m = 6, learn_len 10^6, with two-step records: 0.030 at p = 0.01, where H1 rows
+// hold D_t 98% of the time and the launch takes 529 instead of 617 ms; 0.070 at
+// p = 0.02: 614 vs 631; 0.32 at p = 0.05: 1,023 vs 680 -- a lane that leaves its walk
+// waits for an ACS step of its wave, and those run with few lanes; profiles/r03i_walk/).  CVD_WALK=0 / 1
 // forces it off / on (timing studies; the sums are the same).  Counts-only early decision
 // stays lockstep unless forced: there walk mode measured slower (p = 0.01: 700 vs 648 ms
 // per 2,621,440-trial launch, profiles/r03i_walk/bench_early_walk.json).
 bool cvd::walk_preferred(const cvd_model& M, bool early) {
   const int e = env_i("CVD_WALK", -1);
   if (e >= 0) return e != 0;
-  return !early && M.kind == 1 && M.learn_len_eff > 0 && 25 * M.n_rows < M.learn_len_eff;
+  return !early && M.kind == 1 && M.learn_len_eff > 0 && 10 * M.n_rows < M.learn_len_eff;
 }
 
 int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
@@ -1448,12 +1448,15 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   a.trace = d_trace;
   a.early = early && !d_sums && !d_trace; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
   a.dkey = M.d_dkey;
+  a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
   // lanes), or while < 8 lanes wait for the ACS (profiles/r03i_walk/ab_policy.jsonl)
   a.walk_wmin = env_i("CVD_WALK_WMIN", 48);
   a.walk_amin = env_i("CVD_WALK_AMIN", 8);
-  a.walk_burst = std::max(1, std::min(16, env_i("CVD_WALK_BURST", 16)));   // <= 16 (k1b_walk's word buffer)
+  // <= 16 steps per burst (k1b_walk's word buffer); two-step records: <= 7 iterations of 2
+  a.walk_burst = a.t2 ? std::max(1, std::min(7, env_i("CVD_WALK_BURST", 7)))
+                      : std::max(1, std::min(16, env_i("CVD_WALK_BURST", 16)));
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
   if (which == CVD_KERNEL_BUTTERFLY_RTC) {
     void* args[] = {&a};
@@ -1489,6 +1492,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_hrow, M.h_row))) return rc;
     if ((rc = dev_copy(M.d_drow, M.h_drow))) return rc;
     if ((rc = dev_copy(M.d_dkey, M.h_dkey))) return rc;
+    if ((rc = dev_copy(M.d_t2, M.h_t2))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
     if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
     if ((rc = dev_copy(M.d_bfly, M.bfly))) return rc;
@@ -1515,12 +1519,13 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_bmp, M.d_bmk1,
-                  M.d_bfly};
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
+                  M.d_bmk1, M.d_bfly};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
-  M.d_filt = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_bmp = nullptr;
+  M.d_filt = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_t2 = nullptr;
+  M.d_bmp = nullptr;
   M.d_bmk1 = nullptr;
   M.d_bfly = nullptr;
   M.rtc_fn = nullptr;

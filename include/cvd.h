@@ -87,7 +87,7 @@ typedef struct cvd_model_info {
                               large tables is slower than the two-kernel pipeline) */
   int32_t walk;            /* 1: the specialised m = 6 kernel runs this model's H1 waves in walk mode
                               (learned-row steps from the row records, no ACS; sums unchanged): the
-                              model's rows / learn_len < 1/25, i.e. H1 stays in learned rows (CVD_WALK
+                              model's rows / learn_len < 1/10, i.e. H1 stays in learned rows (CVD_WALK
                               overrides; traces and, unless CVD_WALK=1, counts-only early decision
                               run lockstep) */
 } cvd_model_info;

@@ -85,14 +85,14 @@ def test_walk_early_decision_counts(pkg, monkeypatch, p):
 
 
 def test_walk_flag_follows_row_share(pkg, monkeypatch):
-    """cvd_model_info.walk: on where the model's rows / learn_len < 1/25 (H1 stays in rows),
+    """cvd_model_info.walk: on where the model's rows / learn_len < 1/10 (H1 stays in rows),
     off elsewhere and for dense models; CVD_WALK forces it."""
     cc, det = _m6(pkg)
     monkeypatch.delenv("CVD_WALK", raising=False)
     lo = det.model(0.01, 1_000_000, 200, 1.0, SEED).info()
     hi = det.model(0.1, 1_000_000, 200, 1.0, SEED).info()
-    assert 25 * lo["n_rows"] < lo["learn_len_eff"] and lo["walk"] == 1
-    assert 25 * hi["n_rows"] >= hi["learn_len_eff"] and hi["walk"] == 0
+    assert 10 * lo["n_rows"] < lo["learn_len_eff"] and lo["walk"] == 1
+    assert 10 * hi["n_rows"] >= hi["learn_len_eff"] and hi["walk"] == 0
     monkeypatch.setenv("CVD_WALK", "1")
     assert det.model(0.1, 1_000_000, 200, 1.0, SEED).info()["walk"] == 1
     m2 = pkg.CONFIG_CODES["m2"]
