@@ -223,6 +223,12 @@ __device__ __forceinline__ void fill_filter_patterns() {
 #ifndef CVD_K1B_CMP64
 #define CVD_K1B_CMP64 0
 #endif
+#ifndef CVD_K1B_CMPX
+#define CVD_K1B_CMPX 1
+#endif
+#ifndef CVD_K1B_CMPX_WALK
+#define CVD_K1B_CMPX_WALK CVD_K1B_CMPX
+#endif
 
 // Lookup of the P̂1 row of the current metric state.  A learned row's record
 // holds the row of its successor for every received word, so a sequence that
@@ -321,12 +327,16 @@ struct RowCursor {
     asm volatile("" : "+v"(d));
     return d == 0u;
   }
-  // stored (canonical) key x == lazy key y - kmu8?  Default: subtract, xor and or
-  // per word.  CVD_K1B_CMP64=1: y's words are x + kmu8 with no carry out of any
+  // stored (canonical) key x == lazy key y - kmu8?  Default (CVD_K1B_CMPX=1): the
+  // differences, below; 14 VALU instead of 20 for subtract, xor and or per word
+  // (CVD_K1B_CMPX=0): p = 0.1 710.1 -> 703.6 ms, p = 0.05 680.7 -> 675.6, p = 0.2 686.7 ->
+  // 680.5 per 655,360-trial launch, p <= 0.02 (walk mode) within +-1.7 ms
+  // (profiles/r03o/ab_cmpx.jsonl, profiles/r03p/ab_cmpx_walk.jsonl).  CVD_K1B_CMP64=1: y's words are x + kmu8 with no carry out of any
   // nibble (nibbles <= 14 + 2), so as 64-bit word pairs y = x + K exactly, K = kmu8 *
   // (2^32 + 1): one 64-bit add and one 64-bit compare per pair.  Fewer VALU in the
   // filter-positive block, but measured neutral (p = 0.1: 710.2 vs 709.3 ms per
   // 655,360-trial launch, profiles/r03b/ab_cmp64.jsonl), so it stays off.
+  template <bool kX = CVD_K1B_CMPX>
   __device__ static bool same_key_lazy(const uint32_t (&x)[NW], const uint32_t (&y)[NW], uint32_t kmu8) {
 #if CVD_K1B_CMP64
     if constexpr (NW % 2 == 0) {
@@ -341,6 +351,22 @@ struct RowCursor {
       return eq;
     }
 #endif
+    // y = x + kmu8 word by word (no borrow: every nibble of y is >= its offset) iff
+    // every difference y_w - x_w is kmu8: one subtraction per word, then one v_bitop3
+    // per word pair, (d0 ^ k) | (d1 ^ k) (truth table 0x7E), and an or-reduction
+    if constexpr (kX && NW % 2 == 0) {
+      uint32_t t[NW / 2];
+#pragma unroll
+      for (int i = 0; i < NW / 2; ++i) {
+        const uint32_t d0 = y[2 * i] - x[2 * i], d1 = y[2 * i + 1] - x[2 * i + 1];
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x7e" : "=v"(t[i]) : "v"(d0), "v"(d1), "v"(kmu8));
+      }
+      uint32_t d = 0u;
+#pragma unroll
+      for (int i = 0; i < NW / 2; ++i) d |= t[i];
+      asm volatile("" : "+v"(d));
+      return d == 0u;
+    }
     uint32_t key[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) key[w] = y[w] - kmu8;
@@ -350,6 +376,7 @@ struct RowCursor {
   // kmu8: the stored key is the canonical key + kmu8 in every nibble (lazy
   // normalisation, CVD_K1B_LAZYKEY); subtracted only where the key is compared
   // or hashed
+  template <bool kX = CVD_K1B_CMPX>
   __device__ double resolve(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t r, uint32_t kmu8 = 0u) {
     double lpv = a.lp_unseen;
     if (CVD_ABL & 1) return lpv;
@@ -357,7 +384,7 @@ struct RowCursor {
     if (slot >= 0) {
       lpv = plp; ns = pnx;
     } else if (cand) {
-      if (same_key_lazy(pkey, key_in, kmu8)) {
+      if (same_key_lazy<kX>(pkey, key_in, kmu8)) {
         lpv = plp; ns = (CVD_ABL & 16) ? -2 : pnx;
       } else if (pkey[0] != kEmptyKey) {
         uint32_t key[NW];
@@ -789,7 +816,7 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
     if (mode == kWalkAcs) {
       cur.fence(zn);
       cur.template fence_keys<NW>(zn);
-      lp += cur.resolve(a, key, rr, kmu8);   // Pd_plotter.py:115, T = P̂1
+      lp += cur.template resolve<CVD_K1B_CMPX_WALK>(a, key, rr, kmu8);   // Pd_plotter.py:115, T = P̂1
       constexpr int NH = NW / 2;
       const uint32_t pm = (uint32_t)__builtin_amdgcn_sbfe(6, rr, 1);
       uint32_t hx = 0u, sym = 0u;

@@ -1451,9 +1451,11 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
-  // lanes), or while < 8 lanes wait for the ACS (profiles/r03i_walk/ab_policy.jsonl)
+  // lanes), or while < 4 lanes wait for the ACS (profiles/r03i_walk/ab_policy.jsonl; with
+  // two-step records amin 4 instead of 8: p = 0.01 527.1 -> 524.9 ms, p = 0.02 612.3 -> 610.5
+  // per 655,360-trial launch, profiles/r03p/ab_sched2.jsonl)
   a.walk_wmin = env_i("CVD_WALK_WMIN", 48);
-  a.walk_amin = env_i("CVD_WALK_AMIN", 8);
+  a.walk_amin = env_i("CVD_WALK_AMIN", 4);
   // <= 16 steps per burst (k1b_walk's word buffer); two-step records: <= 7 iterations of 2
   a.walk_burst = a.t2 ? std::max(1, std::min(7, env_i("CVD_WALK_BURST", 7)))
                       : std::max(1, std::min(16, env_i("CVD_WALK_BURST", 16)));
