@@ -951,6 +951,11 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
   static_assert(m >= 3, "k1b kernel: 2^m >= 8 (whole key words)");
   __shared__ double s_lt[R + 1];
   if (threadIdx.x <= R) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+#if defined(CVD_K1B_LDS_PAD) && CVD_K1B_LDS_PAD > 0
+  // timing studies only: LDS padding that lowers the blocks per CU (waves per SIMD)
+  __shared__ uint32_t s_pad[CVD_K1B_LDS_PAD / 4];
+  if (a.N < 0) s_pad[threadIdx.x] = 0u;
+#endif
   fill_filter_patterns();
   if constexpr (kSpec) fill_wtab();
   __syncthreads();
