@@ -226,6 +226,14 @@ __device__ __forceinline__ void fill_filter_patterns() {
 #ifndef CVD_K1B_CMPX
 #define CVD_K1B_CMPX 1
 #endif
+// log P̂1 of an unvisited row held in a VGPR pair across the step loop (the lockstep
+// body's resolve selects it with v_cndmask; from its SGPRs each step first copied it
+// into VGPRs, two v_mov per step): 211 -> 209 static VALU per step, still 126 VGPRs;
+// p = 0.05 / 0.1 / 0.2 675.5 / 705.6 / 678.7 -> 674.1 / 703.8 / 676.3 ms per 655,360-trial
+// launch, walk-mode p within 1 ms (profiles/r03v/ab_lpu.jsonl)
+#ifndef CVD_K1B_LPU_VGPR
+#define CVD_K1B_LPU_VGPR 1
+#endif
 #ifndef CVD_K1B_CMPX_WALK
 #define CVD_K1B_CMPX_WALK CVD_K1B_CMPX
 #endif
@@ -377,8 +385,9 @@ struct RowCursor {
   // normalisation, CVD_K1B_LAZYKEY); subtracted only where the key is compared
   // or hashed
   template <bool kX = CVD_K1B_CMPX>
-  __device__ double resolve(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t r, uint32_t kmu8 = 0u) {
-    double lpv = a.lp_unseen;
+  __device__ double resolve(const ExpArgs& a, const uint32_t (&key_in)[NW], uint32_t r, uint32_t kmu8 = 0u,
+                            const double* unseen = nullptr) {
+    double lpv = unseen ? *unseen : a.lp_unseen;
     if (CVD_ABL & 1) return lpv;
     int32_t ns = -2;
     if (slot >= 0) {
@@ -997,6 +1006,8 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     uint32_t O = 0u, O8 = 0u;   // O8 = O * 0x11111111 (table-driven kernel)
     uint32_t mu_prev = 0u;      // step minimum of D_{t-1} (specialised kernel)
     uint32_t kmu8 = kSpec && CVD_K1B_LAZYKEY ? 0x11111111u : 0u;   // nibble offset of the stored key
+    double lpu = a.lp_unseen;
+    if (CVD_K1B_LPU_VGPR) asm volatile("" : "+v"(lpu));
     if constexpr (kTrace) k1b_trace<m>(a.trace, 0, a.nseq, qwave + lane_id(), key);
     // Received words: word w of this sequence at rbase + (w/4)*cstride + w%4
     // (16-byte chunks, include/cvd.h).  A lane reads its whole chunk at once
@@ -1049,7 +1060,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
       // P̂1 row of D_{t-1}
       cur.fence(zn);                          // zn depends on the whole ACS
       cur.template fence_keys<NW>(zn);
-      lp += cur.resolve(a, key, rr, kmu8);    // Pd_plotter.py:115, T = P̂1
+      lp += cur.resolve(a, key, rr, kmu8, CVD_K1B_LPU_VGPR ? &lpu : nullptr);    // Pd_plotter.py:115, T = P̂1
       // halves differences of D_{t-1}: nibble of state j (< 2^(m-1)) is nonzero
       // iff D_{t-1}(j) != D_{t-1}(j + 2^(m-1))
       constexpr int NH = NW >= 2 ? NW / 2 : 1;
