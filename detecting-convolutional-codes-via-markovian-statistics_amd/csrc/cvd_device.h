@@ -230,7 +230,7 @@ __device__ __forceinline__ void fill_filter_patterns() {
 // body's resolve selects it with v_cndmask; from its SGPRs each step first copied it
 // into VGPRs, two v_mov per step): 211 -> 209 static VALU per step, still 126 VGPRs;
 // p = 0.05 / 0.1 / 0.2 675.5 / 705.6 / 678.7 -> 674.1 / 703.8 / 676.3 ms per 655,360-trial
-// launch, walk-mode p within 1 ms (profiles/r03v/ab_lpu.jsonl)
+// launch, walk-mode p within 1 ms (profiles/r03v/ab_lpu.txt)
 #ifndef CVD_K1B_LPU_VGPR
 #define CVD_K1B_LPU_VGPR 1
 #endif
