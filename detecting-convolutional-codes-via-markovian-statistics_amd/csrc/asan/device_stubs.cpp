@@ -13,6 +13,7 @@ void cvd::free_model_device(cvd_model&) {}
 int cvd::explicit_kernel_of(const cvd_model& M) { return M.k1b_ok ? CVD_KERNEL_BUTTERFLY : CVD_KERNEL_NONE; }
 bool cvd::mc_fused_preferred(const cvd_model&) { return false; }
 bool cvd::walk_preferred(const cvd_model&, bool) { return false; }
+bool cvd::ldsf_preferred(const cvd_model&) { return false; }
 int cvd::device_learn_sparse(const CodeDesc&, int64_t, int64_t, uint64_t, double, int, void*, std::vector<uint8_t>&,
                              std::vector<int64_t>&, int64_t&, LearnStats*) {
   cvd::set_error("no device in the host sanitizer build");

@@ -26,6 +26,20 @@ using cvd::row_words_c;
 using cvd::key_hash;
 
 constexpr int kBlock = 256;
+// LDS-resident Bloom filter (walking models, cvd_kernels.hip): the specialised kernel
+// copies the filter into dynamic LDS at block start and tests it there; its blocks have
+// CVD_K1B_BLOCK threads (the host launches them so)
+#ifndef CVD_K1B_LDSF
+#define CVD_K1B_LDSF 0
+#endif
+#ifndef CVD_K1B_BLOCK
+#define CVD_K1B_BLOCK 256
+#endif
+constexpr int kK1bBlock = CVD_K1B_BLOCK;
+__device__ __forceinline__ uint32_t* dyn_lds() {
+  extern __shared__ uint32_t s_dyn[];
+  return s_dyn;
+}
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 // Uniform read-only tables go through the constant address space so that
@@ -216,7 +230,8 @@ __device__ __forceinline__ void fill_filter_patterns() {
 // differ): bit 0 drops the P̂1 row lookup, bit 1 the T_ref count, bit 2 the
 // hashed lookup of states outside the learned rows (table mode only), bit 4 the
 // table walk after a hashed hit (the lane hashes again), bit 5 the key and record
-// reads of filter-positive lanes (hash and filter test only).
+// reads of filter-positive lanes (hash and filter test only), bit 6 the filter read of the
+// waves of H2 sequences (their lookups end negative).
 #ifndef CVD_ABL
 #define CVD_ABL 0
 #endif
@@ -255,6 +270,7 @@ struct RowCursor {
   static_assert(RSB == 16u * R, "record = one 16-byte entry per received word");
   int32_t slot, pnx;
   uint32_t hs, fb, fw, fb1, fw1;   // filter block words and their patterns
+  bool h2wave = false;             // (CVD_ABL & 64 timing studies: the wave holds H2 sequences only)
   bool cand;
   double plp;
   uint32_t pc;                     // T_ref count c of the entry (kC loads only: the walk mode of k1b_walk)
@@ -438,7 +454,14 @@ struct RowCursor {
                                                        (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 3)));
       fb = pp.x;
       fb1 = pp.y;
+      if (CVD_ABL & 64) {   // timing only: waves of H2 sequences skip the filter read (never a candidate)
+        if (h2wave) { fw = 0u; fw1 = 0u; return; }
+      }
+#if CVD_K1B_LDSF
+      const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + (pl & a.fmask4));
+#else
       const uint2 f = ld_off<uint2>(a.filt, pl & a.fmask4);
+#endif
       fw = f.x;
       fw1 = f.y;
     }
@@ -967,11 +990,19 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
 #endif
   fill_filter_patterns();
   if constexpr (kSpec) fill_wtab();
+#if CVD_K1B_LDSF
+  if constexpr (kSpec) {   // the whole filter, 2 (fmask + 1) words, into dynamic LDS
+    uint4* d = reinterpret_cast<uint4*>(dyn_lds());
+    const uint4* g = reinterpret_cast<const uint4*>(a.filt);
+    for (uint32_t i = threadIdx.x; i < (a.fmask + 1u) / 2u; i += blockDim.x) d[i] = g[i];
+  }
+#endif
   __syncthreads();
   // Sequence index without a VGPR live across the step loop: the wave's first
   // index in SGPRs, the lane from mbcnt, recomputed after the loop; validity
   // and hypothesis as wave ballots (SGPRs)
-  int64_t gw = (int64_t)blockIdx.x * (kBlock / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
+  constexpr int kBlk = kSpec ? kK1bBlock : kBlock;
+  int64_t gw = (int64_t)blockIdx.x * (kBlk / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
   if (!kTrace && a.walk) {
     // H1 and H2 waves alternate (the pair order flips with the block), so every SIMD
     // holds both: the walks' load latency hides under the H2 waves' ACS
@@ -1035,6 +1066,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     int64_t w = 0;                  // index of the current word
     RowCursor<NW, R> cur;
     cur.start(a, cw & 3u);
+    if (CVD_ABL & 64) cur.h2wave = hmask == 0u;
 
     // one step t (1-based) with received word rr and the next step's word rn;
     // the specialised kernel alternates no-broadcast (layout 0 -> 1) and

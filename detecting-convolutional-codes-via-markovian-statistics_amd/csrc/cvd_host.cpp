@@ -509,12 +509,22 @@ void build_hash(cvd_model& Mo) {
   // slower per launch than 2 MiB, profiles/r02h/filter.jsonl).
   // (CVD_FILTER_SCALE=s: filter words >= rows * 2^s, CVD_FILTER_MAX_LOG2: the
   // cap, for timing studies)
-  int fscale = 0, fmax_log2 = 19;
+  // Walking models of <= 32,768 rows (p = 0.01 in the sweep: 29,626): 2^14 words, 64 KiB,
+  // so that the specialised kernel keeps the whole filter in LDS (ldsf_preferred,
+  // cvd_kernels.hip): up to 4 keys per two-word block, ~0.06% false positives, against an
+  // L2 read per H2 step.
+  const bool ldsf = walk_preferred(Mo) && Mo.n_rows <= kLdsFilterMaxRows && !std::getenv("CVD_NO_LDSF");
+  int fscale = 0, fmax_log2 = ldsf ? kLdsFilterLog2 : 19;
   if (const char* e = std::getenv("CVD_FILTER_SCALE")) fscale = std::max(-3, std::min(3, std::atoi(e)));
   if (const char* e = std::getenv("CVD_FILTER_MAX_LOG2")) fmax_log2 = std::max(8, std::min(28, std::atoi(e)));
   while ((fscale >= 0 ? fcap >> fscale : fcap << -fscale) < Mo.n_rows && fcap < ((int64_t)1 << fmax_log2)) fcap <<= 1;
   Mo.fcap = fcap;
   Mo.h_filt.assign((size_t)fcap, 0u);
+  Mo.h_filt_lds.assign(ldsf ? (size_t)fcap : 0u, 0u);
+  // pattern table size (timing studies: CVD_FILTER_PAT_BITS here and, as a JIT define, in
+  // the kernel -- the two must agree)
+  unsigned npat = (unsigned)kFilterPatterns;
+  if (const char* e = std::getenv("CVD_FILTER_PAT_BITS")) npat = 1u << std::max(6, std::min(14, std::atoi(e)));
   Mo.h_key.assign((size_t)cap * ssw, kEmptyKey);
   Mo.h_row.assign(interleave ? 0 : (size_t)cap * Mo.h_rsw, 0u);
   Mo.h_drow.assign((size_t)Mo.n_rows * Mo.h_rsw, 0u);
@@ -550,8 +560,13 @@ void build_hash(cvd_model& Mo) {
     const uint32_t* kw = kws.data() + (size_t)i * nw;
     const uint32_t ph = phs[(size_t)i], pl = pls[(size_t)i];
     const size_t fb = (size_t)filter_block_index(pl, (uint32_t)(fcap / 2 - 1));
-    Mo.h_filt[2 * fb] |= filter_pattern(filter_pattern_index(ph));
-    Mo.h_filt[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph));
+    Mo.h_filt[2 * fb] |= filter_pattern(filter_pattern_index(ph, npat));
+    Mo.h_filt[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph, npat), npat);
+    if (ldsf) {
+      const unsigned nl = 1u << kFilterPatBitsLds;
+      Mo.h_filt_lds[2 * fb] |= filter_pattern(filter_pattern_index(ph, nl));
+      Mo.h_filt_lds[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph, nl), nl);
+    }
     uint64_t slot = ph & (uint64_t)(cap - 1);
     int probe = 0;
     while (Mo.h_key[slot * ssw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
@@ -1084,6 +1099,8 @@ extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
   info->explicit_kernel = explicit_kernel_of(*Mo);
   info->mc_fused = mc_fused_preferred(*Mo) ? 1 : 0;
   info->walk = Mo->k1b_ok && Mo->hcap > 0 && walk_preferred(*Mo) ? 1 : 0;
+  info->lds_filter = Mo->device >= 0 ? (Mo->rtc_fn && Mo->rtc_ldsf ? 1 : 0)
+                                     : (Mo->k1b_ok && Mo->hcap > 0 && ldsf_preferred(*Mo) ? 1 : 0);
   return CVD_OK;
 }
 

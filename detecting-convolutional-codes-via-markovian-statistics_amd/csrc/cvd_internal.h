@@ -35,6 +35,7 @@ struct cvd_model {
   int32_t max_probe = 0;
   std::vector<int64_t> row_next;  // [n_rows][2^n] row index of successor(row, r), -1 if not a row
   std::vector<uint32_t> h_filt;   // [fcap] blocked Bloom filter words (filter_pattern)
+  std::vector<uint32_t> h_filt_lds;   // the same filter with 2^kFilterPatBitsLds patterns (LDS kernel), or empty
   int64_t fcap = 0;               // filter words, power of two
   std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector, word 0 = kEmptyKey if empty
   int32_t h_rsw = 0;              // row record stride in dwords (row_words)
@@ -58,6 +59,8 @@ struct cvd_model {
   uint32_t bfly_even[4] = {0, 0, 0, 0};   // nibble masks of the butterflies j with out(j, 0) in {00, 11}
   uint64_t bfly_x = 0;             // out(j, 0) in bits 2j..2j+1 (the specialisation key)
   void* rtc_fn = nullptr;          // hipFunction_t of the specialised kernel on `device`, if built
+  int rtc_block = 256;             // its block size (1,024 with the LDS-resident filter)
+  bool rtc_ldsf = false;           // it reads the Bloom filter from dynamic LDS (fcap * 4 bytes)
   std::string jit_error;           // why the specialised kernel is unavailable (empty if built or n/a)
   std::vector<uint32_t> bfly;      // [2^m / 2]
 
@@ -67,6 +70,7 @@ struct cvd_model {
   double* d_logp1 = nullptr;
   double* d_ltref = nullptr;
   uint32_t* d_filt = nullptr;
+  uint32_t* d_filt_lds = nullptr;
   uint32_t* d_hkey = nullptr;
   uint32_t* d_hrow = nullptr;
   uint32_t* d_drow = nullptr;
@@ -101,6 +105,12 @@ int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int6
 bool mc_fused_preferred(const cvd_model& M);
 // the specialised butterfly kernel runs the model's H1 waves in walk mode (k1b_walk)
 bool walk_preferred(const cvd_model& M, bool early = false);
+// LDS-resident Bloom filter of the specialised kernel: walking models of at most
+// kLdsFilterMaxRows rows, whose filter is built with 2^kLdsFilterLog2 words (64 KiB, <= 4
+// keys per two-word block, ~0.06% false positives) for 512-thread blocks, two per CU
+constexpr int kLdsFilterLog2 = 14;
+constexpr int64_t kLdsFilterMaxRows = 32768;
+bool ldsf_preferred(const cvd_model& M);
 int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
                     uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,
                     int64_t* d_counts, void* stream, bool early);
@@ -115,7 +125,7 @@ int explicit_kernel_of(const cvd_model& M);
 // hipRTC-compiled code-specialised butterfly kernel (cvd_rtc.cpp); 0 = ok
 // CVD_OK if the model is uploaded to the current device
 int check_device(const cvd_model& M);
-int rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out);
+int rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, void** fn_out);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);
 

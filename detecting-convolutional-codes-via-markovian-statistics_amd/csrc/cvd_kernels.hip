@@ -1416,6 +1416,21 @@ static int env_i(const char* name, int def) {
 // forces it off / on (timing studies; the sums are the same).  Counts-only early decision
 // stays lockstep unless forced: there walk mode measured slower (p = 0.01: 700 vs 648 ms
 // per 2,621,440-trial launch, profiles/r03i_walk/bench_early_walk.json).
+// The specialised kernel reads the Bloom filter from LDS (CVD_K1B_LDSF, 512-thread blocks, two
+// per CU) for walking models of <= 32,768 rows, whose filter is built with 64 KiB: in walk mode
+// the H2 waves are two per SIMD and their per-step filter read from L2 is what they wait on
+// (profiles/r03w: skipping it, timing only, takes p = 0.01 524 -> 466 ms per 655,360-trial
+// launch).  Measured (profiles/r03x/ab_block.jsonl, ms per 655,360-trial launch, p = 0.01 /
+// 0.02): 256-thread blocks, global filter 531.5 / 612.3; 512 threads, LDS filter of 64 KiB
+// 502.4 / 619.4 (p = 0.02's 70,134 rows pass ~3% of non-rows at that size); 1,024 threads, LDS
+// filter of 128 KiB 543.8 / 643.4 (blocks of 16 waves wait for their slowest wave: 1,024
+// threads with the global filter 570.9 / 668.7, 512 threads 541.6 / 625.7).  CVD_NO_LDSF=1
+// keeps the filter in global memory.
+bool cvd::ldsf_preferred(const cvd_model& M) {
+  return !std::getenv("CVD_NO_LDSF") && walk_preferred(M) && M.n_rows <= kLdsFilterMaxRows &&
+         M.fcap <= ((int64_t)1 << kLdsFilterLog2) && M.h_filt_lds.size() == (size_t)M.fcap;
+}
+
 bool cvd::walk_preferred(const cvd_model& M, bool early) {
   const int e = env_i("CVD_WALK", -1);
   if (e >= 0) return e != 0;
@@ -1434,7 +1449,9 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   }
   if (nseq <= 0) return CVD_OK;
   ExpArgs a;
-  a.filt = M.d_filt; a.hkey = M.d_hkey; a.drow = M.d_drow; a.ltref = M.d_ltref;
+  // (the LDS-filter kernel copies its own filter copy, the one with its smaller pattern table)
+  a.filt = which == CVD_KERNEL_BUTTERFLY_RTC && M.rtc_ldsf ? M.d_filt_lds : M.d_filt;
+  a.hkey = M.d_hkey; a.drow = M.d_drow; a.ltref = M.d_ltref;
   // directory slots: keys [hcap][h_ssw dwords], records [hcap][h_rsw] or, interleaved
   // (no separate record array), at dword nw of each key slot
   a.hrow = M.d_hrow ? M.d_hrow : M.d_hkey + nib_words(M.dec.m);
@@ -1462,7 +1479,9 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
   if (which == CVD_KERNEL_BUTTERFLY_RTC) {
     void* args[] = {&a};
-    HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M.rtc_fn, grid, 1, 1, kBlock, 1, 1, 0,
+    const unsigned blk = (unsigned)M.rtc_block, rgrid = (unsigned)((nseq + blk - 1) / blk);
+    const unsigned lds = M.rtc_ldsf ? (unsigned)(M.fcap * sizeof(uint32_t)) : 0u;   // the filter (CVD_K1B_LDSF)
+    HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M.rtc_fn, rgrid, 1, 1, blk, 1, 1, lds,
                                     (hipStream_t)stream, args, nullptr));
     return CVD_OK;
   }
@@ -1490,6 +1509,7 @@ int cvd::upload_model(cvd_model& M, int device) {
   }
   if (M.hcap > 0) {
     if ((rc = dev_copy(M.d_filt, M.h_filt))) return rc;
+    if ((rc = dev_copy(M.d_filt_lds, M.h_filt_lds))) return rc;
     if ((rc = dev_copy(M.d_hkey, M.h_key))) return rc;
     if ((rc = dev_copy(M.d_hrow, M.h_row))) return rc;
     if ((rc = dev_copy(M.d_drow, M.h_drow))) return rc;
@@ -1509,8 +1529,17 @@ int cvd::upload_model(cvd_model& M, int device) {
   // cvd_model_jit_status
   M.rtc_fn = nullptr;
   M.jit_error.clear();
-  if (M.k1b_ok && M.hcap > 0 && rtc_k1b_function(device, M.dec.m, M.bfly_x, &M.rtc_fn) != 0) {
+  M.rtc_ldsf = M.k1b_ok && M.hcap > 0 && ldsf_preferred(M);
+  // block size: 512 threads with the LDS filter (two blocks of 8 waves per CU hold it),
+  // else 256 (CVD_K1B_BLOCK=256/512/1024 overrides, timing studies)
+  M.rtc_block = env_i("CVD_K1B_BLOCK", M.rtc_ldsf ? 512 : kBlock);
+  if (M.rtc_block != 256 && M.rtc_block != 512 && M.rtc_block != 1024) M.rtc_block = kBlock;
+  const std::string vdefs = "-DCVD_K1B_BLOCK=" + std::to_string(M.rtc_block) +
+                            (M.rtc_ldsf ? " -DCVD_K1B_LDSF=1 -DCVD_FILTER_PAT_BITS=" + std::to_string(kFilterPatBitsLds) : "");
+  if (M.k1b_ok && M.hcap > 0 && rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn) != 0) {
     M.rtc_fn = nullptr;
+    M.rtc_ldsf = false;
+    M.rtc_block = kBlock;
     M.jit_error = last_error_copy();
   }
   return CVD_OK;
@@ -1521,12 +1550,12 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_filt_lds, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
                   M.d_bmk1, M.d_bfly};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
-  M.d_filt = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_t2 = nullptr;
+  M.d_filt = nullptr; M.d_filt_lds = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_t2 = nullptr;
   M.d_bmp = nullptr;
   M.d_bmk1 = nullptr;
   M.d_bfly = nullptr;

@@ -78,13 +78,21 @@ CVD_HD void key_hash_less(const unsigned* w, int nw, unsigned c, unsigned& ph, u
 // 32-bit words) per key, a pattern of three bits in each word.  A lookup of a
 // state that is not a row (most lookups at p >= 0.05 and for every H2 sequence)
 // ends on this one L2-resident 8-byte load.  The pattern pair comes from a table
-// of kFilterPatterns entries indexed by bits 3..14 of ph (the device keeps it in
+// of kFilterPatterns entries indexed by bits 3..12 of ph (the device keeps it in
 // LDS as 64-bit entries: one AND gives the byte offset, one LDS read the pair,
 // instead of the shifts and ors of six bit positions).  Two words with three
 // bits each pass a non-row ~10x less often than one word at the same filter size
 // (p = 0.2, ~1.9 rows per 32-bit word: ~0.4% -> ~0.04%), and every false
-// positive is a directory line read.
-constexpr int kFilterPatBits = 12, kFilterPatterns = 1 << kFilterPatBits;
+// positive is a directory line read.  4,096 pattern pairs (32 KiB of LDS).  The kernel
+// variant with the filter itself in LDS (walking models) builds a second copy of the
+// filter with 1,024 pattern pairs (8 KiB, CVD_FILTER_PAT_BITS=10 in that kernel) to make
+// room; 1,024 for every filter measured +1.6% / +2.5% per launch at p = 0.1 / 0.2, where
+// a two-word block holds 3-4 keys (profiles/r03z/ab_pat.jsonl).
+#ifndef CVD_FILTER_PAT_BITS
+#define CVD_FILTER_PAT_BITS 12
+#endif
+constexpr int kFilterPatBits = CVD_FILTER_PAT_BITS, kFilterPatterns = 1 << kFilterPatBits;
+constexpr int kFilterPatBitsLds = 10;
 CVD_HD unsigned filter_pattern(unsigned i) {
   unsigned x = (i + 1u) * 0x9E3779B1u;
   x ^= x >> 15;
@@ -97,8 +105,9 @@ CVD_HD unsigned filter_pattern(unsigned i) {
   return (1u << b0) | (1u << b1) | (1u << b2);
 }
 // pattern pair i: low word filter_pattern(i), high word filter_pattern(i + kFilterPatterns)
-CVD_HD unsigned filter_pattern_hi(unsigned i) { return filter_pattern(i + (unsigned)kFilterPatterns); }
-CVD_HD unsigned filter_pattern_index(unsigned ph) { return (ph >> 3) & (unsigned)(kFilterPatterns - 1); }
+// (npat: the table size, kFilterPatterns unless a timing study overrides it on both sides)
+CVD_HD unsigned filter_pattern_hi(unsigned i, unsigned npat = kFilterPatterns) { return filter_pattern(i + npat); }
+CVD_HD unsigned filter_pattern_index(unsigned ph, unsigned npat = kFilterPatterns) { return (ph >> 3) & (npat - 1u); }
 // block index (words 2b, 2b + 1); bmask = blocks - 1 (the device takes the
 // block's byte offset as pl & (bmask << 3))
 CVD_HD unsigned filter_block_index(unsigned pl, unsigned bmask) { return (pl >> 3) & bmask; }

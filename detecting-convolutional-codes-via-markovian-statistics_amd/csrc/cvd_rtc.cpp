@@ -97,7 +97,7 @@ const char* kClangFlags[] = {"-O3", "-std=c++17", "-ffp-contract=off",
 std::string entry_source(int m, uint64_t xm) {
   char entry[256];
   std::snprintf(entry, sizeof(entry),
-                "\nextern \"C\" __global__ __launch_bounds__(cvd_dev::kBlock, cvd_dev::kK1bWavesPerSimd)\n"
+                "\nextern \"C\" __global__ __launch_bounds__(cvd_dev::kK1bBlock, cvd_dev::kK1bWavesPerSimd)\n"
                 "void cvd_k1b_spec(cvd_dev::ExpArgs a) { cvd_dev::k1b_body<%d, true, 0x%016llxull, false>(a); }\n",
                 m, (unsigned long long)xm);
   return entry;
@@ -120,7 +120,8 @@ std::string find_clang() {
 }
 
 // device-only compile with the toolchain clang -> code object bytes
-bool compile_clang(const std::string& src, const std::string& arch, std::vector<char>& code, std::string& err) {
+bool compile_clang(const std::string& src, const std::string& arch, const std::string& defs, std::vector<char>& code,
+                   std::string& err) {
   const std::string clang = find_clang();
   if (clang.empty()) { err = "no clang++ found (set CVD_JIT_CLANG)"; return false; }
   char dir_t[] = "/tmp/cvd_jit_XXXXXX";
@@ -135,8 +136,8 @@ bool compile_clang(const std::string& src, const std::string& arch, std::vector<
   std::vector<std::string> args = {clang, "-x", "hip", arch_opt, "--offload-device-only", "--no-gpu-bundle-output"};
   for (const char* f : kClangFlags) args.push_back(f);
   for (const char* f : {"-c", in.c_str(), "-o", out.c_str()}) args.push_back(f);
-  if (const char* d = std::getenv("CVD_JIT_DEFINES")) {   // tuning experiments: -D and -mllvm <opt> only
-    std::istringstream ds(d);
+  {   // the model's variant and tuning experiments (CVD_JIT_DEFINES): -D and -mllvm <opt> only
+    std::istringstream ds(defs);
     std::string t, o;
     while (ds >> t) {
       if (t.rfind("-D", 0) == 0) {
@@ -175,8 +176,22 @@ bool compile_clang(const std::string& src, const std::string& arch, std::vector<
   return ok;
 }
 
-bool compile_hiprtc(const std::string& src, const std::string& arch, std::vector<char>& code, std::string& err) {
+bool compile_hiprtc(const std::string& src0, const std::string& arch, const std::string& defs, std::vector<char>& code,
+                    std::string& err) {
   hiprtcProgram prog;
+  // the -D defines as #define lines (hipRTC takes no -mllvm options here)
+  std::string src;
+  {
+    std::istringstream ds(defs);
+    std::string t;
+    while (ds >> t)
+      if (t.rfind("-D", 0) == 0) {
+        const std::string d = t.substr(2);
+        const size_t eq = d.find('=');
+        src += "#define " + (eq == std::string::npos ? d + " 1" : d.substr(0, eq) + " " + d.substr(eq + 1)) + "\n";
+      }
+  }
+  src += src0;
   if (hiprtcCreateProgram(&prog, src.c_str(), "cvd_k1b_spec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
     err = "hiprtcCreateProgram failed";
     return false;
@@ -204,13 +219,15 @@ bool compile_hiprtc(const std::string& src, const std::string& arch, std::vector
 }  // namespace
 
 // hipFunction_t of cvd_k1b_spec<m, code> on `device`, compiling it on first use.
-int cvd::rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out) {
+int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, void** fn_out) {
   *fn_out = nullptr;
   if (const char* e = std::getenv("CVD_NO_JIT"))
     if (e[0] && e[0] != '0') { set_error("JIT: disabled by CVD_NO_JIT"); return -1; }
   std::lock_guard<std::mutex> lock(g_mu);
-  const char* defs = std::getenv("CVD_JIT_DEFINES");
-  const auto key = std::make_tuple(device, m, xm, std::string(defs ? defs : ""));
+  // the model's variant (e.g. the LDS-resident filter) before the tuning defines
+  const char* env_defs = std::getenv("CVD_JIT_DEFINES");
+  const std::string all_defs = std::string(variant_defs ? variant_defs : "") + " " + (env_defs ? env_defs : "");
+  const auto key = std::make_tuple(device, m, xm, all_defs);
   auto it = g_cache.find(key);
   if (it != g_cache.end()) {
     *fn_out = (void*)it->second;
@@ -231,7 +248,7 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out) {
   std::string cpath;
   if (!force_rtc) {
     const std::string dir = cache_dir();
-    std::string keytxt = src + "\n" + arch + "\n" + find_clang() + "\n" + (defs ? defs : "");
+    std::string keytxt = src + "\n" + arch + "\n" + find_clang() + "\n" + all_defs;
     for (const char* f : kClangFlags) keytxt += std::string("\n") + f;
     if (!dir.empty()) {
       char name[64];
@@ -258,9 +275,9 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, void** fn_out) {
     }
     ::unlink(cpath.c_str());   // unusable cached object: rebuild it
   }
-  bool ok = !force_rtc && compile_clang(src, arch, code, err1);
+  bool ok = !force_rtc && compile_clang(src, arch, all_defs, code, err1);
   if (ok && !cpath.empty()) cache_store(cpath, code);
-  if (!ok) ok = compile_hiprtc(src, arch, code, err2);
+  if (!ok) ok = compile_hiprtc(src, arch, all_defs, code, err2);
   if (!ok) { set_error("JIT: " + err1 + " | " + err2); return -1; }
   if (!load(fn)) { set_error("JIT: module load failed"); return -1; }
   g_cache[key] = fn;   // modules live for the process (one per device and code)

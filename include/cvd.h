@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 6
+#define CVD_ABI_VERSION 7
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -90,6 +90,9 @@ typedef struct cvd_model_info {
                               model's rows / learn_len < 1/10, i.e. H1 stays in learned rows (CVD_WALK
                               overrides; traces and, unless CVD_WALK=1, counts-only early decision
                               run lockstep) */
+  int32_t lds_filter;      /* 1: the specialised kernel keeps this model's Bloom filter in LDS (walking
+                              models of <= 32,768 rows, filter built with 64 KiB, 512-thread blocks;
+                              CVD_NO_LDSF=1 keeps it in global memory) */
 } cvd_model_info;
 
 #define CVD_KERNEL_NONE 0       /* explicit path unsupported for this shape */

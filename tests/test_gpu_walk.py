@@ -99,3 +99,28 @@ def test_walk_flag_follows_row_share(pkg, monkeypatch):
     d2 = pkg.Detector(1, 2, 2, m2["gen1"], device=0)
     monkeypatch.delenv("CVD_WALK")
     assert d2.model(0.05, None, 200, 1.0, SEED).info()["walk"] == 0
+
+
+def test_lds_filter_equals_global_filter(pkg, monkeypatch):
+    """cvd_model_info.lds_filter: walking models of <= 32,768 rows keep a 64 KiB Bloom filter
+    in LDS (512-thread blocks); the sums equal the global-filter kernel's (CVD_NO_LDSF=1,
+    256-thread blocks, the filter sized >= 32 bits per row) and the lockstep run's."""
+    cc, det = _m6(pkg)
+    p, N, t0, t1 = 0.01, 3001, 17, 17 + 700
+    monkeypatch.delenv("CVD_WALK", raising=False)
+    monkeypatch.delenv("CVD_NO_LDSF", raising=False)
+    # fresh models (Detector.model keeps one per key): the filter is sized at build, the
+    # kernel variant chosen at upload
+    lds = pkg.Model(det.dec, p, 300_000, 200, 1.0, SEED).upload(0)
+    assert lds.info()["walk"] == 1 and lds.info()["lds_filter"] == 1
+    got, gc = _sums(det, lds, cc, N, p, t0, t1)
+    monkeypatch.setenv("CVD_NO_LDSF", "1")
+    glob = pkg.Model(det.dec, p, 300_000, 200, 1.0, SEED).upload(0)
+    assert glob.info()["lds_filter"] == 0
+    ref, rc = _sums(det, glob, cc, N, p, t0, t1)
+    monkeypatch.delenv("CVD_NO_LDSF")
+    monkeypatch.setenv("CVD_WALK", "0")
+    lock, lc = _sums(det, lds, cc, N, p, t0, t1)
+    assert np.array_equal(got, ref) and np.array_equal(lock, ref)
+    assert gc == rc == lc
+    assert pkg.Model(det.dec, 0.1, 300_000, 200, 1.0, SEED).upload(0).info()["lds_filter"] == 0
