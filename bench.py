@@ -433,6 +433,8 @@ def main():
                        "generator_pmc": gen_pmc,
                        # walk mode of the m = 6 kernel per grid point (cvd_model_info.walk)
                        "walk_by_p": {str(p): int(models[p].info().get("walk", 0)) for p in p_grid} if models else None,
+                       "lds_filter_by_p": ({str(p): int(models[p].info().get("lds_filter", 0)) for p in p_grid}
+                                           if models else None),
                        "per_p": per_p},
     }
     if early_out is not None:
