@@ -5,6 +5,8 @@ Per-trial fp64 sums and counts must equal the lockstep kernel's (CVD_WALK=0) bit
 bit -- and the C oracle's -- at every p of the sweep, for trial counts that are not
 whole waves (one wave mixes H1 and H2 lanes), N not a multiple of the 16-step word,
 and every schedule extreme (burst of one step, always / never preferring walks)."""
+import warnings
+
 import numpy as np
 import pytest
 
@@ -124,3 +126,33 @@ def test_lds_filter_equals_global_filter(pkg, monkeypatch):
     assert np.array_equal(got, ref) and np.array_equal(lock, ref)
     assert gc == rc == lc
     assert pkg.Model(det.dec, 0.1, 300_000, 200, 1.0, SEED).upload(0).info()["lds_filter"] == 0
+
+
+@pytest.mark.parametrize("how", ["hiprtc", "nojit"])
+def test_lds_filter_model_under_jit_fallbacks(pkg, monkeypatch, how):
+    """A model built for the LDS-filter kernel (walking, <= 32,768 rows) stays exact when the
+    kernel comes from the hipRTC fallback (the variant's -D defines become #define lines) or
+    when there is no specialised kernel at all (the library's table-driven butterfly kernel
+    reads the global filter copy with the 4,096-pattern table)."""
+    cc, det = _m6(pkg)
+    p, N, t0, t1 = 0.01, 2500, 5, 5 + 320
+    for v in ("CVD_WALK", "CVD_NO_LDSF", "CVD_JIT_VIA", "CVD_NO_JIT"):
+        monkeypatch.delenv(v, raising=False)
+    ref_model = pkg.Model(det.dec, p, 300_000, 200, 1.0, SEED).upload(0)
+    assert ref_model.info()["lds_filter"] == 1
+    ref, rc = _sums(det, ref_model, cc, N, p, t0, t1)
+    if how == "hiprtc":
+        monkeypatch.setenv("CVD_JIT_VIA", "hiprtc")
+    else:
+        monkeypatch.setenv("CVD_NO_JIT", "1")
+    with warnings.catch_warnings():   # (no JIT: upload warns that the table-driven kernel runs)
+        warnings.simplefilter("ignore", RuntimeWarning)
+        alt = pkg.Model(det.dec, p, 300_000, 200, 1.0, SEED).upload(0)
+    inf = alt.info()
+    if how == "hiprtc":
+        assert inf["explicit_kernel"] == 4 and inf["lds_filter"] == 1
+    else:
+        assert inf["explicit_kernel"] == 3 and inf["lds_filter"] == 0
+    got, gc = _sums(det, alt, cc, N, p, t0, t1)
+    assert np.array_equal(got, ref)
+    assert gc == rc
