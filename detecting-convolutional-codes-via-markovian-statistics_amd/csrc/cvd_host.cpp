@@ -521,10 +521,7 @@ void build_hash(cvd_model& Mo) {
   Mo.fcap = fcap;
   Mo.h_filt.assign((size_t)fcap, 0u);
   Mo.h_filt_lds.assign(ldsf ? (size_t)fcap : 0u, 0u);
-  // pattern table size (timing studies: CVD_FILTER_PAT_BITS here and, as a JIT define, in
-  // the kernel -- the two must agree)
-  unsigned npat = (unsigned)kFilterPatterns;
-  if (const char* e = std::getenv("CVD_FILTER_PAT_BITS")) npat = 1u << std::max(6, std::min(14, std::atoi(e)));
+  const unsigned npat = (unsigned)kFilterPatterns;   // the kernels' pattern table (cvd_keys.h)
   Mo.h_key.assign((size_t)cap * ssw, kEmptyKey);
   Mo.h_row.assign(interleave ? 0 : (size_t)cap * Mo.h_rsw, 0u);
   Mo.h_drow.assign((size_t)Mo.n_rows * Mo.h_rsw, 0u);

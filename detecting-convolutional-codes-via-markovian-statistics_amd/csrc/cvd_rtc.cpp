@@ -224,9 +224,20 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
   if (const char* e = std::getenv("CVD_NO_JIT"))
     if (e[0] && e[0] != '0') { set_error("JIT: disabled by CVD_NO_JIT"); return -1; }
   std::lock_guard<std::mutex> lock(g_mu);
-  // the model's variant (e.g. the LDS-resident filter) before the tuning defines
-  const char* env_defs = std::getenv("CVD_JIT_DEFINES");
-  const std::string all_defs = std::string(variant_defs ? variant_defs : "") + " " + (env_defs ? env_defs : "");
+  // the model's variant (e.g. the LDS-resident filter) before the tuning defines; the
+  // variant's own macros (block size, LDS filter, pattern table) are the host's to set --
+  // the launch geometry and the filter copy follow them -- so CVD_JIT_DEFINES cannot
+  // override them
+  std::string env_defs;
+  if (const char* e = std::getenv("CVD_JIT_DEFINES")) {
+    std::istringstream ds(e);
+    std::string t;
+    while (ds >> t)
+      if (t.rfind("-DCVD_K1B_BLOCK", 0) != 0 && t.rfind("-DCVD_K1B_LDSF", 0) != 0 &&
+          t.rfind("-DCVD_FILTER_PAT_BITS", 0) != 0)
+        env_defs += " " + t;
+  }
+  const std::string all_defs = std::string(variant_defs ? variant_defs : "") + env_defs;
   const auto key = std::make_tuple(device, m, xm, all_defs);
   auto it = g_cache.find(key);
   if (it != g_cache.end()) {

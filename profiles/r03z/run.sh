@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 3: filter pattern table of 1,024 entries (8 KiB) against 4,096 (32 KiB), global filter,
-# the lockstep p of the sweep (the host build and the JIT kernel use the same table size)
+# the lockstep p of the sweep (the host build and the JIT kernel use the same table size; run
+# on the tree before commit bfbbee3, where CVD_FILTER_PAT_BITS was a host env knob and a JIT define)
 set -uo pipefail
 O=gpurun_out/r03z
 mkdir -p $O
