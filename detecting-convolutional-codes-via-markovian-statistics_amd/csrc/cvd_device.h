@@ -355,8 +355,9 @@ struct RowCursor {
   // differences, below; 14 VALU instead of 20 for subtract, xor and or per word
   // (CVD_K1B_CMPX=0): p = 0.1 710.1 -> 703.6 ms, p = 0.05 680.7 -> 675.6, p = 0.2 686.7 ->
   // 680.5 per 655,360-trial launch, p <= 0.02 (walk mode) within +-1.7 ms
-  // (profiles/r03o/ab_cmpx.jsonl, profiles/r03p/ab_cmpx_walk.jsonl).  CVD_K1B_CMP64=1: y's words are x + kmu8 with no carry out of any
-  // nibble (nibbles <= 14 + 2), so as 64-bit word pairs y = x + K exactly, K = kmu8 *
+  // (profiles/r03o/ab_cmpx.jsonl, profiles/r03p/ab_cmpx_walk.jsonl).  CVD_K1B_CMP64=1:
+  // y's words are x + kmu8 with no carry out of any nibble (nibbles <= 14 + 2), so as
+  // 64-bit word pairs y = x + K exactly, K = kmu8 *
   // (2^32 + 1): one 64-bit add and one 64-bit compare per pair.  Fewer VALU in the
   // filter-positive block, but measured neutral (p = 0.1: 710.2 vs 709.3 ms per
   // 655,360-trial launch, profiles/r03b/ab_cmp64.jsonl), so it stays off.
