@@ -6,13 +6,15 @@ Pd match vs CPU".  Workload (configs[2]): the m = 6 pair (133,171) vs (171,133),
 N = 1e5, p swept over {0.01, 0.02, 0.05, 0.10, 0.15, 0.20}.
 
 One trial = one H1 plus one H2 sequence of length N (one iteration of
-Pd_plotter.py:210-223).  One step = one batch of `--batch` trials per GPU at
-one p of the sweep (step s uses p_grid[s % 6]): the generator kernel writes the
-batch's BSC-noised received streams to HBM (encoder + Philox noise, two
-launches: H1 with G1, H2 with G2), then the detector kernel reads them
-(Eq. 4-5 recursion, T_ref count, hashed P̂1 row lookup, fp64 log-likelihood
-sums, decisions, counts).  Both kernels are inside the timed region; learning
-P̂1 (host setup, once per p) is not.
+Pd_plotter.py:210-223).  One step = one pass over the config's p grid with
+`--batch` trials per GPU at EVERY p (Pd_plotter.py:199-233 runs num_iter trials
+at every p, so the sweep's p weigh equally whatever --steps is): per p the
+generator kernel writes the batch's BSC-noised received streams to HBM (encoder
++ Philox noise, two launches: H1 with G1, H2 with G2), then the detector kernels
+read them (Eq. 4-5 recursion, T_ref count, hashed P̂1 row lookup, fp64
+log-likelihood sums, decisions, counts), the step's detector launches spread
+over `--streams` device queues.  Both kernels are inside the timed region;
+learning P̂1 (host setup, once per p) is not.
 
 Multi-GPU: one process per GPU, rank r takes its own global trial ids every
 step (weak scaling); the success counts are reduced with one RCCL all_reduce
@@ -85,7 +87,12 @@ def parse():
                          "evenly over the (N, p) grid points like the reference's num_iter per point")
     ap.add_argument("--c4-N", default="1000,10000,100000,1000000", help="c4: the N grid (Pd_plotter.py:196)")
     ap.add_argument("--N", type=int, default=None)
-    ap.add_argument("--batch", type=int, default=None, help="trials per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="trials per GPU per p per step (a step runs every p of the config's grid)")
+    ap.add_argument("--multi", type=int, default=1,
+                    help="detect a step's grid points in multi-model launches (cvd_detect_multi: the models "
+                         "that share the specialised kernel variant in ONE launch, so the step pays one "
+                         "last-round tail instead of one per p); 0: one launch per p")
     ap.add_argument("--learn-len", type=int, default=1_000_000,
                     help="P̂1 learning chain length for non-enumerable codes")
     ap.add_argument("--seed", type=int, default=12345)
@@ -189,15 +196,15 @@ def main():
         models = dict(zip(p_grid, det.prepare_models(p_grid, a.learn_len if m == 6 else None, 200, 1.0, a.seed)))
         info = models[p_grid[0]].info()
     t_setup = time.perf_counter() - t_setup
-    # whole residency rounds: 4 waves/SIMD x 1024 SIMDs x 64 lanes = 262,144 sequences
-    # (131,072 trials) per round.  m6: 20 rounds per launch (131 GB of streams) -- the
-    # last round's uneven wave finish costs ~24 ms per launch, amortised over the rounds
-    # (DESIGN.md "Launch size": 687k trials/s at 2 rounds, 735k at 10, 742k at 20)
-    # m2: 2^22 trials (56.0M vs 52.3M trials/s at 2^20); r23_m4: 2^17 measured best
-    B = a.batch or {"m6": 2_621_440, "m2": 4_194_304, "r23_m4": 131_072}[a.config]
-    # double-buffered pipeline: the generator fills buffer (s+1)%2 on its own
-    # stream while the detector reads buffer s%2 (both kernels of every timed
-    # step run inside the timed region)
+    # One step = one pass over the config's whole p grid (Pd_plotter.py:199-233 runs num_iter
+    # trials at every p): B trials per GPU at EVERY p, so the sweep's p are weighted equally
+    # whatever --steps is.  Whole residency rounds per launch: 4 waves/SIMD x 1024 SIMDs x 64
+    # lanes = 262,144 sequences (131,072 trials) per round.  m6: 3 rounds per p (2,359,296
+    # trials and 118 GB of streams per step); the six detector launches of a step run on
+    # --streams device queues, so one launch's last-round tail is filled by the next
+    # launch's waves (DESIGN.md "Measurement").  m2: 2^22 trials (one p); r23_m4: 2^17 per p.
+    B = a.batch or {"m6": 393_216, "m2": 4_194_304, "r23_m4": 131_072}[a.config]
+    npg = len(p_grid)
     if a.fused < 0:
         a.fused = int(not parity and bool(info["mc_fused"]))   # where it measured faster (cvd_model_info)
     if a.fused:
@@ -207,19 +214,29 @@ def main():
     buf_bytes = det.words_per_seq(N) * 4 * 2 * B
     if a.overlap and 2 * buf_bytes > (120 << 30):
         a.overlap = 0                          # two batches would not leave HBM headroom
-    nbuf = 2 if a.overlap else 1
-    bufs = [] if a.fused else [det.stream_buffer(N, 2 * B) for _ in range(nbuf)]
-    counts = torch.zeros((len(p_grid), 2), dtype=torch.int64, device=det.device)
-    dstream = torch.cuda.current_stream()
-    gstream = torch.cuda.Stream(device=det.device) if a.overlap else dstream
+    # units: unit u of the run is grid point p_grid[u % npg] of step u // npg.  Overlap
+    # (table automaton): double-buffered generator on its own stream; otherwise one buffer
+    # per grid point, the step's generator launches first, then its detector launches --
+    # with --multi, the grid points whose models share the specialised kernel variant in
+    # one launch each (cvd_detect_multi; m6: p = 0.01 with its LDS filter, then the other
+    # five).  (Concurrent per-p launches on 2, 3 or 6 device queues measured 0.3%, 12% and
+    # 8% slower than one queue: the models' tables compete for the caches, profiles/r04a/.)
+    nbuf = 0 if a.fused else (2 if a.overlap else npg)
+    bufs = [det.stream_buffer(N, 2 * B) for _ in range(nbuf)]
+    counts = torch.zeros((npg, 2), dtype=torch.int64, device=det.device)
+    main = torch.cuda.current_stream()
+    gstream = torch.cuda.Stream(device=det.device) if a.overlap else main
+    use_multi = bool(a.multi) and not (a.overlap or a.fused or parity)
+    groups = det.multi_groups([models[p] for p in p_grid]) if use_multi else [[i] for i in range(npg)]
 
-    def gen(s, ev=None):
+    def gen(u, ev=None):
         if a.fused:
             return   # the fused kernel generates its own words (detect below)
-        p = p_grid[s % len(p_grid)]
-        tb = (s * world + rank) * B            # global trial ids of this rank's batch
+        s, i = divmod(u, npg)
+        p = p_grid[i]
+        tb = (s * world + rank) * B            # global trial ids of this rank's batch at this p
         tag = pkg.grid_tag(N, p)
-        r = bufs[s % nbuf]
+        r = bufs[u % nbuf]
         if ev is not None:
             ev[0].record(gstream)
         det.generate(g1, N, p, a.seed, tag, 2 * tb, 2, B, out=r, q0=0, pitch=2 * B, stream=gstream)
@@ -229,46 +246,65 @@ def main():
 
     early = [False]
 
-    def detect(s, ev=None):
-        p = p_grid[s % len(p_grid)]
+    def detect(u0, grp, st, ev=None):
+        """grid points grp (indices into p_grid) of the step starting at unit u0"""
         if ev is not None:
-            ev[2].record(dstream)
-        if parity:
-            pkg.parity_detect(bufs[s % nbuf], n, N, 2 * B, B, tpl, a.gamma, counts=counts[s % len(p_grid)],
-                              stream=dstream)
-        elif a.fused:
-            tb = (s * world + rank) * B            # global trial ids of this rank's batch
-            det.run_trials(models[p], cc["gen1"], cc["gen2"], N, p, a.seed, tb, tb + B,
-                           counts=counts[s % len(p_grid)], stream=dstream, early_decision=early[0], fused=True)
+            ev[0].record(st)
+        if len(grp) > 1:
+            det.detect_multi([models[p_grid[i]] for i in grp], [bufs[(u0 + i) % nbuf] for i in grp], N,
+                             [2 * B] * len(grp), [B] * len(grp), [counts[i] for i in grp], stream=st,
+                             early_decision=early[0])
         else:
-            det.detect(models[p], bufs[s % nbuf], N, 2 * B, B, counts=counts[s % len(p_grid)], stream=dstream,
-                       early_decision=early[0])
+            i = grp[0]
+            u = u0 + i
+            s = u // npg
+            p = p_grid[i]
+            if parity:
+                pkg.parity_detect(bufs[u % nbuf], n, N, 2 * B, B, tpl, a.gamma, counts=counts[i], stream=st)
+            elif a.fused:
+                tb = (s * world + rank) * B
+                det.run_trials(models[p], cc["gen1"], cc["gen2"], N, p, a.seed, tb, tb + B,
+                               counts=counts[i], stream=st, early_decision=early[0], fused=True)
+            else:
+                det.detect(models[p], bufs[u % nbuf], N, 2 * B, B, counts=counts[i], stream=st,
+                           early_decision=early[0])
         if ev is not None:
-            ev[3].record(dstream)
+            ev[1].record(st)
 
-    def run(steps, base, events=None):
+    def run(steps, base, gev=None, dev=None):
+        """steps whole sweeps from step `base`; gev[u] generator events per unit, dev[s][g]
+        detector events per launch group g of step s"""
         if steps <= 0:
             return
+        u0 = base * npg
+        nu = steps * npg
         if not a.overlap:
             for s in range(steps):
-                ev = events[s] if events else None
-                gen(base + s, ev)
-                detect(base + s, ev)
+                for i in range(npg):
+                    gen(u0 + s * npg + i, gev[s * npg + i] if gev else None)
+                for g, grp in enumerate(groups):
+                    detect(u0 + s * npg, grp, main, dev[s][g] if dev else None)
             return
-        done = [torch.cuda.Event() for _ in range(steps)]
-        ready = [torch.cuda.Event() for _ in range(steps)]
-        gen(base, events[0] if events else None)
+        done = [torch.cuda.Event() for _ in range(nu)]
+        ready = [torch.cuda.Event() for _ in range(nu)]
+        gen(u0, gev[0] if gev else None)
         ready[0].record(gstream)
-        for s in range(steps):
-            dstream.wait_event(ready[s])
-            detect(base + s, events[s] if events else None)
-            done[s].record(dstream)
-            if s + 1 < steps:
-                if s >= 1:
-                    gstream.wait_event(done[s - 1])   # buffer (s+1)%2 was read by detect(s-1)
-                gen(base + s + 1, events[s + 1] if events else None)
-                ready[s + 1].record(gstream)
-        dstream.wait_stream(gstream)
+        for u in range(nu):
+            main.wait_event(ready[u])
+            s, i = divmod(u, npg)
+            detect(u0 + s * npg, [i], main, dev[s][i] if dev else None)
+            done[u].record(main)
+            if u + 1 < nu:
+                if u >= 1:
+                    gstream.wait_event(done[u - 1])   # buffer (u+1)%2 was read by detect(u-1)
+                gen(u0 + u + 1, gev[u + 1] if gev else None)
+                ready[u + 1].record(gstream)
+        main.wait_stream(gstream)
+
+    def make_events(steps):
+        gev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps * npg)]
+        dev = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in groups] for _ in range(steps)]
+        return gev, dev
 
     # warmup steps use trial ids far from the timed ones (base 10,000 steps)
     run(a.warmup, 10_000)
@@ -277,9 +313,9 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(a.steps)]
+    gev, dev = make_events(a.steps)
     t0 = time.perf_counter()
-    run(a.steps, 0, events)
+    run(a.steps, 0, gev, dev)
     if dist:
         dist.all_reduce(counts)                # the one collective: success counts over RCCL
     torch.cuda.synchronize()
@@ -295,9 +331,17 @@ def main():
 
     if dist:
         elapsed = max_over_ranks(elapsed)
-    gen_ms = 0.0 if a.fused else float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    det_each = [e[2].elapsed_time(e[3]) for e in events]
-    det_ms = float(np.mean(det_each))
+    for mdl in models.values():
+        mdl.device_error()                     # raises if a detector launch flagged an error
+    gen_ms = 0.0 if a.fused else float(np.mean([e[0].elapsed_time(e[1]) for e in gev])) * npg
+    # detector launches: per launch group, mean over the steps (ms)
+    grp_ms = [float(np.mean([dev[s][g][0].elapsed_time(dev[s][g][1]) for s in range(a.steps)]))
+              for g in range(len(groups))]
+    phase_ms = float(np.sum(grp_ms))           # the step's detector launches, back to back on one queue
+    # the dominant launch (the roofline's kernel): the group with the most grid points
+    gdom = max(range(len(groups)), key=lambda g: (len(groups[g]), grp_ms[g]))
+    det_ms = grp_ms[gdom]
+    det_by_group = [{"p": [p_grid[i] for i in groups[g]], "ms": grp_ms[g]} for g in range(len(groups))]
 
     # the same steps (same trial ids) with early decision: counts must be identical
     early_out = None
@@ -308,9 +352,9 @@ def main():
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
-        ev2 = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(a.steps)]
+        gev2, dev2 = make_events(a.steps)
         t1 = time.perf_counter()
-        run(a.steps, 0, ev2)
+        run(a.steps, 0, gev2, dev2)
         if dist:
             dist.all_reduce(counts)
         torch.cuda.synchronize()
@@ -321,9 +365,11 @@ def main():
         if dist:
             el2 = max_over_ranks(el2)
         early[0] = False
-        d2 = [e[2].elapsed_time(e[3]) for e in ev2]
-        early_out = {"value": a.steps * B * world / el2, "unit": "trials/s", "ms_per_step": el2 / a.steps * 1e3,
-                     "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): d2[s] for s in range(a.steps)},
+        d2 = [float(np.mean([dev2[s][g][0].elapsed_time(dev2[s][g][1]) for s in range(a.steps)]))
+              for g in range(len(groups))]
+        early_out = {"value": a.steps * npg * B * world / el2, "unit": "trials/s", "ms_per_step": el2 / a.steps * 1e3,
+                     "detector_ms_by_launch": [{"p": [p_grid[i] for i in groups[g]], "ms": d2[g]}
+                                               for g in range(len(groups))],
                      "counts_equal_full_run": bool(torch.equal(counts, full_counts)),
                      "note": "counts only: each trial stops once its decision is certain (rigorous IEEE "
                              "bounds on the remaining increments, CVD_DETECT_EARLY_DECISION); the "
@@ -334,33 +380,44 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    trials = a.steps * B * world
+    trials = a.steps * npg * B * world
     value = trials / elapsed
-    # roofline of the dominant kernel (detector): algorithmic bytes = the packed
-    # received streams read once, 2 * ceil(N * n / 8) bytes per trial
-    alg_bytes = B * 2 * ((N * n + 7) // 8)
-    achieved = alg_bytes / (det_ms * 1e-3) / 1e9
+    # roofline of the dominant kernel (detector): algorithmic bytes = the packed received
+    # streams read once, 2 * ceil(N * n / 8) bytes per trial, per launch of
+    # the dominant launch group (m6: the multi-model launch of five grid points), over that
+    # launch's average duration (HIP events on its stream, the figure rocprofv3 reports)
+    alg_bytes = B * 2 * ((N * n + 7) // 8)               # one grid point's batch
+    alg_launch = len(groups[gdom]) * alg_bytes
+    achieved = alg_launch / (det_ms * 1e-3) / 1e9
     if a.fused:
         # no stream in HBM: the fused kernel is bound by its LDS gathers (per sequence-step
         # one 16-bit record and two f64 entries, 18 B) and the generator's VALU; LDS peak
         # 256 B/clk/CU (MI355X_MICROARCH.md, LDS: ds_read_b64) x 256 CUs x 2.4 GHz
         alg_bytes = B * 2 * N * 18
-        achieved = alg_bytes / (det_ms * 1e-3) / 1e9
+        alg_launch = len(groups[gdom]) * alg_bytes
+        achieved = alg_launch / (det_ms * 1e-3) / 1e9
     traffic, traffic_src, pmc = None, None, None
     if a.pmc_traffic is None:
         a.pmc_traffic = os.path.join(ROOT, "profiles", f"pmc_{a.detector}_{a.config}.json")
     if a.pmc_traffic and os.path.exists(a.pmc_traffic):
         with open(a.pmc_traffic) as f:
             pmc = json.load(f)
-        if (pmc.get("config"), pmc.get("batch"), pmc.get("N"), pmc.get("detector", "markov"),
-                bool(pmc.get("fused", False))) != (a.config, B, N, a.detector, bool(a.fused)) or \
+        if (pmc.get("config"), pmc.get("N"), pmc.get("detector", "markov"),
+                bool(pmc.get("fused", False))) != (a.config, N, a.detector, bool(a.fused)) or \
                 sorted(pmc.get("per_p", {})) != sorted(str(p) for p in p_grid):
             pmc = None   # counters of another workload (or of a single-p diagnostic run)
     valu = None
     traffic_by_p, gen_pmc = None, None
     if pmc is not None:
-        traffic = pmc.get("detector_fetch_bytes_per_launch")   # launch-weighted mean over the sweep
-        traffic_by_p = {p: {"fetch_bytes": e["fetch_bytes"], "fetch_x_algorithmic": e["fetch_x_algorithmic"],
+        # launch-weighted mean over the sweep, per trial of the PMC run's launches (whole
+        # residency rounds like this run's) times this run's trials per launch
+        pmc_scale = B / float(pmc.get("batch") or B)
+        # the dominant launch's traffic: the FETCH of its grid points' single-p launches
+        try:
+            traffic = sum(pmc["per_p"][str(p_grid[i])]["fetch_bytes"] for i in groups[gdom]) * pmc_scale
+        except (KeyError, TypeError):
+            traffic = None
+        traffic_by_p = {p: {"fetch_bytes": e["fetch_bytes"] * pmc_scale, "fetch_x_algorithmic": e["fetch_x_algorithmic"],
                             "fetch_raw_x_algorithmic": e["fetch_raw_x_algorithmic"],
                             "valu_insts_per_wave_step": e["VALU_insts_per_wave_step"],
                             "vmem_rd_insts_per_wave_step": e["VMEM_RD_insts_per_wave_step"]}
@@ -370,13 +427,15 @@ def main():
             gen_pmc = {k: g[k] for k in ("kernel", "fetch_bytes_raw", "VALU_insts_per_wave", "VALU_insts_per_stream_word",
                                          "SALU_insts_per_stream_word", "busy_frac_of_wave_cycles",
                                          "wait_any_frac_of_wave_cycles") if k in g}
-        traffic_src = os.path.relpath(a.pmc_traffic, ROOT) + " (" + pmc.get("traffic_basis", "rocprofv3 FETCH_SIZE") + ")"
+        traffic_src = (os.path.relpath(a.pmc_traffic, ROOT) + " (" + pmc.get("traffic_basis", "rocprofv3 FETCH_SIZE")
+                       + (f"; counted on {pmc.get('batch')}-trial launches, scaled to {B}" if pmc_scale != 1.0 else "")
+                       + ")")
         ipws = pmc.get("VALU_insts_per_wave_step")
         if ipws:
             # VALU roofline of the detector (its binding resource): wave-instructions
             # per launch from the counter pass, over this run's live launch time
-            winst = ipws * (2 * B / 64) * N
-            ach = winst / (det_ms * 1e-3)
+            winst = ipws * (2 * B * npg / 64) * N          # the step's detector launches
+            ach = winst / (phase_ms * 1e-3)
             cpi = pmc.get("valu_cycles_per_inst")
             valu = {"insts_per_wave_step": ipws, "achieved": ach, "peak": VALU_PEAK_WINST,
                     "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WINST,
@@ -385,9 +444,10 @@ def main():
                     "cycles_per_inst": cpi,
                     "issue_cycle_weighted_frac": (ach * cpi / (1024 * SHADER_GHZ * 1e9)) if cpi else None,
                     "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU, opcode mix x "
-                              "profiles/valu_issue_cycles.json) + live HIP-event time"}
+                              "profiles/valu_issue_cycles.json) + live HIP-event time of the detector phase"}
     c = counts.cpu().numpy()
-    per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, (a.steps // len(p_grid) + (i < a.steps % len(p_grid))) * B * world),
+    per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, a.steps * B * world),
+                      "Pc": float(c[i, 0] + c[i, 1]) / max(1, 2 * a.steps * B * world),
                       "h1_successes": int(c[i, 0]), "h2_successes": int(c[i, 1])}
              for i, p in enumerate(p_grid)}
     out = {
@@ -406,8 +466,11 @@ def main():
         "data": "synthetic: Philox4x32-10 encoder inputs and BSC(p) flips (build spec), learned P̂1",
         "config": {"name": a.config, "detector": a.detector,
                    "workload": f"{a.config} pair {cc['gen1']} vs {cc['gen2']}, N={N}, p-sweep {p_grid}, "
-                               f"one p per step", "N": N, "p_grid": p_grid,
-                   "trials_per_step_per_gpu": B, "k": k, "n": n, "m": m,
+                               f"every p in every step ({B} trials per p per GPU)", "N": N, "p_grid": p_grid,
+                   "p_weighting": "equal: each step runs the same trials per GPU at every p of the grid "
+                                  "(Pd_plotter.py:199-233 runs num_iter trials per p)",
+                   "trials_per_p_per_step_per_gpu": B, "trials_per_step_per_gpu": B * npg,
+                   "k": k, "n": n, "m": m,
                    "model": info["kind"] and "sparse(learned)" or "dense",
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
@@ -421,15 +484,18 @@ def main():
                                 else pkg.KERNEL_NAMES[info["explicit_kernel"]] if info["kind"]
                                 else "detect_table_kernel (enumerated state automaton)"),
                      "traffic_source": traffic_src,
-                     "traffic_x_algorithmic": (traffic / alg_bytes) if traffic else None,
+                     "traffic_x_algorithmic": (traffic / alg_launch) if traffic else None,
                      "traffic_by_p": traffic_by_p,
-                     "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": det_ms,
+                     "algorithmic_bytes_per_launch": alg_launch, "avg_launch_ms": det_ms,
+                     "launch_grid_points": [p_grid[i] for i in groups[gdom]],
+                     "detector_launches_per_step": len(groups), "detector_ms_per_step": phase_ms,
+                     "step_achieved": npg * alg_bytes / (phase_ms * 1e-3) / 1e9,
                      "valu": valu},
-        "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": det_ms,
+        "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": phase_ms,
                        "overlap": bool(a.overlap), "fused": bool(a.fused), "model_setup_s": t_setup,
-                       "seq_steps_per_s_detector": 2 * B * N / (det_ms * 1e-3),
-                       "detector_ms_by_p": {str(p_grid[s % len(p_grid)]): det_each[s] for s in range(a.steps)},
-                       "detector_ms_steps": det_each,
+                       "multi_model_launches": use_multi,
+                       "seq_steps_per_s_detector": 2 * B * npg * N / (phase_ms * 1e-3),
+                       "detector_ms_by_launch": det_by_group,
                        "generator_pmc": gen_pmc,
                        # walk mode of the m = 6 kernel per grid point (cvd_model_info.walk)
                        "walk_by_p": {str(p): int(models[p].info().get("walk", 0)) for p in p_grid} if models else None,
@@ -471,7 +537,9 @@ def run_c4(a, pkg, world, rank, local, dist):
     models = dict(zip(p_grid, det.prepare_models(p_grid, a.learn_len, 200, 1.0, a.seed)))
     t_setup = time.perf_counter() - t_setup
     free, _ = torch.cuda.mem_get_info(det.device)
-    budget = min(int(free * 0.6), 131 << 30)         # one batch's streams (the bench's 131 GB at N = 1e5)
+    # one batch's streams: up to 200 GB of the 288 GB, so N = 1e6 launches hold three
+    # residency rounds (393,216 trials, 197 GB) instead of two
+    budget = min(int(free * 0.75), 200 << 30)
 
     def batch_of(N):
         b = det.default_batch(N, hi - lo, budget)
@@ -488,16 +556,22 @@ def run_c4(a, pkg, world, rank, local, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    mlist = [models[p] for p in p_grid]
     for iN, N in enumerate(Ns):
         tn = time.perf_counter()
         B = batch_of(N)
-        for ip, p in enumerate(p_grid):
-            det.run_trials(models[p], cc["gen1"], cc["gen2"], N, p, a.seed, lo, hi, batch=B,
-                           counts=counts[iN, ip], early_decision=False)
-            if N >= 100_000:   # a progress line per long grid point (the launches are queued)
+        if N >= 100_000:
+            # a progress line per long grid point (the launches are queued): one grid call per p
+            for ip, p in enumerate(p_grid):
+                det.run_grid([models[p]], cc["gen1"], cc["gen2"], [p], [N], a.seed, lo, hi, batch=B,
+                             counts=counts[iN, ip].view(1, 1, 2))
                 torch.cuda.synchronize()
                 print(json.dumps({"c4_point": {"rank": rank, "N": N, "p": p, "seconds": time.perf_counter() - tn}}),
                       file=sys.stderr, flush=True)
+        else:
+            # the whole p row of this N in ONE library call (cvd_mc_run_grid)
+            det.run_grid(mlist, cc["gen1"], cc["gen2"], p_grid, [N], a.seed, lo, hi, batch=B,
+                         counts=counts[iN].view(1, len(p_grid), 2))
         torch.cuda.synchronize()
         per_n_s.append(time.perf_counter() - tn)
         print(json.dumps({"c4_progress": {"rank": rank, "N": N, "seconds": per_n_s[-1]}}), file=sys.stderr,
@@ -520,9 +594,22 @@ def run_c4(a, pkg, world, rank, local, dist):
         return
     c = counts.cpu().numpy()
     total = T * npt
+    def roof_N(i, N):
+        # the packed streams read once, 2 ceil(N n / 8) bytes per trial, over
+        # the N's whole pipeline time (generator + detector, max over ranks)
+        ab = T * len(p_grid) * 2 * ((N * n + 7) // 8)
+        ach = ab / per_n_s[i] / 1e9
+        b = batch_of(N)
+        lpp = -(-(hi - lo) // b)                          # launches per grid point on a rank
+        return {"algorithmic_bytes": ab, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ach / HBM_PEAK_GBS, "basis": "whole pipeline time of this N (generator + detector)",
+                "launches_per_point_per_rank": lpp,
+                "residency_rounds_per_launch": b / pkg.Detector.FULL_ROUND_TRIALS,
+                "last_launch_rounds": ((hi - lo) - (lpp - 1) * b) / pkg.Detector.FULL_ROUND_TRIALS}
+
     per_N = {str(N): {"trials": T * len(p_grid), "seconds": per_n_s[i], "trials_per_s": T * len(p_grid) / per_n_s[i],
                       "seq_steps_per_s": 2 * T * len(p_grid) * N / per_n_s[i],
-                      "batch_per_rank": batch_of(N),
+                      "batch_per_rank": batch_of(N), "roofline": roof_N(i, N),
                       "per_p": {str(p): {"h1_successes": int(c[i, j, 0]), "h2_successes": int(c[i, j, 1]),
                                          "Pd": float(c[i, j, 0]) / T, "Pc": float(c[i, j, 0] + c[i, j, 1]) / (2 * T)}
                                 for j, p in enumerate(p_grid)}}
@@ -546,6 +633,12 @@ def run_c4(a, pkg, world, rank, local, dist):
                    "learn_len": a.learn_len, "early_decision": False,
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "per_N": per_N,
+        "roofline": {"bound": "valu", "achieved": sum(per_N[str(N)]["roofline"]["algorithmic_bytes"] for N in Ns)
+                     / elapsed / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": sum(per_N[str(N)]["roofline"]["algorithmic_bytes"] for N in Ns) / elapsed / 1e9 / HBM_PEAK_GBS,
+                     "traffic": None,
+                     "basis": "algorithmic stream bytes of every grid point (SURVEY §8(d)) over the whole timed "
+                              "region (generator + detector); per N in per_N[N].roofline"},
         "counts": c.tolist(),
         "diagnostic": {"model_setup_s": t_setup, "elapsed_s": elapsed},
     }

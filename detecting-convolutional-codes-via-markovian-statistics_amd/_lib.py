@@ -12,7 +12,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5
 DETECT_EARLY_DECISION = 0x100   # OR'ed into path: counts only, stop once every decision is certain
@@ -91,6 +91,9 @@ EXPORTS = {
     "cvd_detect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
                                   ctypes.c_void_p]),
+    "cvd_detect_multi": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int32, ctypes.c_void_p]),
     "cvd_trace": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                  ctypes.c_void_p, ctypes.c_void_p]),
     "cvd_mc_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(cvd_code), ctypes.c_int64, ctypes.c_int64]),
@@ -98,6 +101,13 @@ EXPORTS = {
                                   ctypes.c_double, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_int32, ctypes.c_void_p]),
+    "cvd_mc_grid_workspace_bytes": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(cvd_code),
+                                                     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]),
+    "cvd_mc_run_grid": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_code),
+                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                       ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    "cvd_model_device_error": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
     "cvd_mc_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_code),
                                     ctypes.c_double, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,

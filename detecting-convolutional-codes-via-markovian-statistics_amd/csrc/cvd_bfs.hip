@@ -50,7 +50,7 @@ using namespace cvd_chain;
     hipError_t e_ = (x);                                                                  \
     if (e_ != hipSuccess) {                                                               \
       set_error(std::string("HIP error '") + hipGetErrorString(e_) + "' at " #x);          \
-      return e_ == hipErrorOutOfMemory ? CVD_E_CAPACITY : CVD_E_HIP;                      \
+      return CVD_E_HIP;                                                                   \
     }                                                                                     \
   } while (0)
 
@@ -284,6 +284,10 @@ extern "C" int cvd_enumerate_device(const cvd_code* dec, int32_t device, int64_t
                                     int64_t* S_out, uint8_t* states_out, int32_t* next_out, int64_t* level_sizes,
                                     int32_t max_levels, int32_t* n_levels_out, void* stream) {
   if (!dec || !S_out || cap < 1 || device < 0) { set_error("bad cvd_enumerate_device arguments"); return CVD_E_INVALID; }
+  // CVD_E_CAPACITY always comes with S_out >= 1 (the states certified so far); any other
+  // failure leaves S_out = 0, which no caller may read as a bound
+  *S_out = 0;
+  if (n_levels_out) *n_levels_out = 0;
   if (dec->k < 1 || dec->k > kMaxK || dec->n < 1 || dec->n > kMaxN || dec->m < 1 || dec->m > kMaxM || !dec->taps) {
     set_error("code shape out of range");
     return CVD_E_INVALID;
@@ -329,7 +333,7 @@ extern "C" int cvd_enumerate_device(const cvd_code* dec, int32_t device, int64_t
     if (sc > scap) { scap = sc; slots = sl; }
     if ((double)sl * 0.6 > (double)(cap + 1)) break;
   }
-  if (scap < 2) { set_error("GPU enumeration: not enough device memory"); return CVD_E_CAPACITY; }
+  if (scap < 2) { set_error("GPU enumeration: not enough device memory to start"); return CVD_E_HIP; }
   // staging for a level's new states: all of scap while that is small, half beyond
   const int64_t stage = std::max<int64_t>(1024, scap <= ((int64_t)1 << 26) ? scap : scap / 2);
   DevMem dm;

@@ -173,6 +173,7 @@ struct ExpArgs {
   int32_t walk;             // k1b_walk for H1 waves (specialised kernel; no trace, no early decision, N < 2^31)
   int32_t walk_wmin, walk_amin, walk_burst;   // k1b_walk schedule (see there)
   double lt_min, lp_min;    // smallest log T_ref / log P̂1 increments (early_decide)
+  int32_t* err;             // error flags (nullable): bit 0 = k1b_walk left its loop by the guard
 };
 
 // Received words of one sequence, one word of lookahead (the next step's r is
@@ -964,6 +965,10 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
     acs_step(IntC<1>{});
     acs_step(IntC<2>{});
   }
+  // the guard is never reached (every iteration moves a lane); if a scheduling bug ever
+  // reaches it, the lanes' partial sums must not pass for results: flag it for the host
+  // (cvd_model_device_error), one global atomic from the wave
+  if (__ballot(mode != kWalkDone) != 0u && lane_id() == 0 && a.err) atomicOr(a.err, 1);
   // (CVD_WALK_ABL & 2: schedule statistics of the first H1 waves, printed; sums unchanged)
   if ((CVD_WALK_ABL & 2) && qwave < 4 * 64 * 4 && lane_id() == 0)
     printf("walkstats q0=%lld acs_pairs=%lld lanes_per_acs=%.1f bursts=%lld burst_iters=%lld walkers_per_burst=%.1f unpacks=%lld\n",
@@ -978,8 +983,10 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
   count_decisions_masked(vmask, vmask, lp, lr, a.counts);
 }
 
+// blk: the block's index within this model's launch range (blockIdx.x, or its offset in a
+// multi-model launch, k1b_multi)
 template <int m, bool kSpec, uint64_t XM, bool kTrace>
-__device__ __forceinline__ void k1b_body(const ExpArgs& a) {
+__device__ __forceinline__ void k1b_body(const ExpArgs& a, uint32_t blk) {
   constexpr int M = 1 << m, H = M / 2, NW = M / 8, R = 4;
   static_assert(m >= 3, "k1b kernel: 2^m >= 8 (whole key words)");
   __shared__ double s_lt[R + 1];
@@ -1003,7 +1010,7 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
   // index in SGPRs, the lane from mbcnt, recomputed after the loop; validity
   // and hypothesis as wave ballots (SGPRs)
   constexpr int kBlk = kSpec ? kK1bBlock : kBlock;
-  int64_t gw = (int64_t)blockIdx.x * (kBlk / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
+  int64_t gw = (int64_t)blk * (kBlk / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
   if (!kTrace && a.walk) {
     // H1 and H2 waves alternate (the pair order flips with the block), so every SIMD
     // holds both: the walks' load latency hides under the H2 waves' ACS
@@ -1186,6 +1193,34 @@ __device__ __forceinline__ void k1b_body(const ExpArgs& a) {
     early_final(dec, lp, lr);
   }
   count_decisions_masked(vmask, hmask, lp, lr, a.counts);
+}
+
+// ──────── several models in ONE launch (cvd_detect_multi; specialised kernel) ────────
+//
+// A p sweep detects one batch per model (one learned P̂1 per p, Pd_plotter.py:123-169,
+// 199-233).  Launched one model at a time, every launch ends with a last residency round
+// whose waves finish unevenly (their row lookups differ), which costs ~15-25 ms per
+// launch at N = 1e5 (DESIGN.md "Measurement").  Here consecutive block ranges run
+// consecutive models -- blocks [blk_end[i-1], blk_end[i]) model i -- so the dispatcher
+// starts model i+1's blocks in the CUs model i's last waves leave idle, and a step pays one
+// tail instead of one per p.  Blocks are dispatched in order, so at any time the resident
+// waves belong to one model or, at a boundary, two: their tables share the caches no
+// worse than one model's (concurrent launches of several models on separate queues
+// measured 12% slower, profiles/r04a/).  Every model of a launch shares the decoder code
+// (the kernel is specialised to it) and the variant (block size, LDS filter).
+constexpr int kMultiMax = 8;
+struct MultiArgs {
+  ExpArgs a[kMultiMax];
+  uint32_t blk_end[kMultiMax];   // cumulative block counts
+  int32_t nm;
+};
+template <int m, uint64_t XM>
+__device__ __forceinline__ void k1b_multi(const MultiArgs& ma) {
+  const uint32_t b = blockIdx.x;
+  int i = 0;
+  uint32_t b0 = 0u;
+  while (i + 1 < ma.nm && b >= ma.blk_end[i]) b0 = ma.blk_end[i++];   // scalar: blockIdx is uniform
+  k1b_body<m, true, XM, false>(ma.a[i], b - b0);
 }
 
 }  // namespace cvd_dev

@@ -987,11 +987,10 @@ extern "C" int cvd_model_save(const cvd_model* Mo, const char* path) {
   w.vec(Mo->ltref); w.vec(Mo->keys); w.vec(Mo->logp1); w.vec(Mo->rec); w.vec(Mo->rowsum);
   w.vec(Mo->p1_nz); w.vec(Mo->row_next); w.vec(Mo->visits);
   const bool ok = w.ok && std::fclose(f) == 0;
+  // (a rename onto an existing file is atomic on POSIX: concurrent writers of one cache
+  // entry never fail here, so a failure is real -- EACCES, EXDEV, ... -- and is reported)
   if (!ok || std::rename(tmp.c_str(), path) != 0) {
     std::remove(tmp.c_str());
-    // another writer's rename may have won the race: its file is the same model
-    struct stat sb;
-    if (ok && stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) return CVD_OK;
     set_error(std::string("cannot write ") + path);
     return CVD_E_INVALID;
   }
@@ -1095,7 +1094,9 @@ extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
   info->logp1_unseen = Mo->logp1_unseen;
   info->explicit_kernel = explicit_kernel_of(*Mo);
   info->mc_fused = mc_fused_preferred(*Mo) ? 1 : 0;
-  info->walk = Mo->k1b_ok && Mo->hcap > 0 && walk_preferred(*Mo) ? 1 : 0;
+  // walk mode runs only on the specialised kernel: once uploaded, report what runs (no JIT
+  // kernel -> lockstep), before upload what would
+  info->walk = Mo->k1b_ok && Mo->hcap > 0 && walk_preferred(*Mo) && (Mo->device < 0 || Mo->rtc_fn) ? 1 : 0;
   info->lds_filter = Mo->device >= 0 ? (Mo->rtc_fn && Mo->rtc_ldsf ? 1 : 0)
                                      : (Mo->k1b_ok && Mo->hcap > 0 && ldsf_preferred(*Mo) ? 1 : 0);
   return CVD_OK;

@@ -59,6 +59,7 @@ struct cvd_model {
   uint32_t bfly_even[4] = {0, 0, 0, 0};   // nibble masks of the butterflies j with out(j, 0) in {00, 11}
   uint64_t bfly_x = 0;             // out(j, 0) in bits 2j..2j+1 (the specialisation key)
   void* rtc_fn = nullptr;          // hipFunction_t of the specialised kernel on `device`, if built
+  void* rtc_fn_multi = nullptr;    // its multi-model entry (cvd_detect_multi), same module
   int rtc_block = 256;             // its block size (1,024 with the LDS-resident filter)
   bool rtc_ldsf = false;           // it reads the Bloom filter from dynamic LDS (fcap * 4 bytes)
   std::string jit_error;           // why the specialised kernel is unavailable (empty if built or n/a)
@@ -79,6 +80,7 @@ struct cvd_model {
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
   uint32_t* d_bfly = nullptr;
+  int32_t* d_err = nullptr;       // kernel error flags (k1b_walk's scheduler guard), cvd_model_device_error
 };
 
 namespace cvd {
@@ -125,7 +127,8 @@ int explicit_kernel_of(const cvd_model& M);
 // hipRTC-compiled code-specialised butterfly kernel (cvd_rtc.cpp); 0 = ok
 // CVD_OK if the model is uploaded to the current device
 int check_device(const cvd_model& M);
-int rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, void** fn_out);
+int rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, void** fn_out,
+                     void** fn_multi_out = nullptr);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);
 

@@ -1148,7 +1148,7 @@ __global__ __launch_bounds__(kBlock, kK1WavesPerSimd) void detect_k1_kernel(ExpA
 // per-code table (cvd_device.h); hipRTC builds the code-specialised variant
 template <int m, bool kTrace>
 __global__ __launch_bounds__(kBlock, kK1bWavesPerSimd) void detect_k1b_kernel(ExpArgs a) {
-  k1b_body<m, false, 0, kTrace>(a);
+  k1b_body<m, false, 0, kTrace>(a, blockIdx.x);
 }
 
 using ExpKernel = void (*)(ExpArgs);
@@ -1437,17 +1437,9 @@ bool cvd::walk_preferred(const cvd_model& M, bool early) {
   return !early && M.kind == 1 && M.learn_len_eff > 0 && 10 * M.n_rows < M.learn_len_eff;
 }
 
-int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
-                                int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
-                                void* stream, int variant, bool early) {
-  ExpKernel kern = nullptr;
-  const uint32_t* bmp = nullptr;
-  const int which = select_explicit(M, variant, &kern, &bmp, d_trace != nullptr);
-  if (which == CVD_KERNEL_NONE || !M.d_filt || !bmp) {
-    set_error("explicit path: unsupported code shape (m,k,n)");
-    return CVD_E_UNSUPPORTED;
-  }
-  if (nseq <= 0) return CVD_OK;
+// The explicit path's launch arguments of one model over one stream buffer.
+static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int64_t N, int64_t nseq, int64_t n_h1,
+                        double* d_sums, int64_t* d_counts, uint8_t* d_trace, const uint32_t* bmp, bool early) {
   ExpArgs a;
   // (the LDS-filter kernel copies its own filter copy, the one with its smaller pattern table)
   a.filt = which == CVD_KERNEL_BUTTERFLY_RTC && M.rtc_ldsf ? M.d_filt_lds : M.d_filt;
@@ -1465,6 +1457,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   a.trace = d_trace;
   a.early = early && !d_sums && !d_trace; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
   a.dkey = M.d_dkey;
+  a.err = M.d_err;
   a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
@@ -1476,6 +1469,21 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   // <= 16 steps per burst (k1b_walk's word buffer); two-step records: <= 7 iterations of 2
   a.walk_burst = a.t2 ? std::max(1, std::min(7, env_i("CVD_WALK_BURST", 7)))
                       : std::max(1, std::min(16, env_i("CVD_WALK_BURST", 16)));
+  return a;
+}
+
+int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
+                                int64_t n_h1, double* d_sums, int64_t* d_counts, uint8_t* d_trace,
+                                void* stream, int variant, bool early) {
+  ExpKernel kern = nullptr;
+  const uint32_t* bmp = nullptr;
+  const int which = select_explicit(M, variant, &kern, &bmp, d_trace != nullptr);
+  if (which == CVD_KERNEL_NONE || !M.d_filt || !bmp) {
+    set_error("explicit path: unsupported code shape (m,k,n)");
+    return CVD_E_UNSUPPORTED;
+  }
+  if (nseq <= 0) return CVD_OK;
+  ExpArgs a = exp_args(M, which, d_r, N, nseq, n_h1, d_sums, d_counts, d_trace, bmp, early);
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
   if (which == CVD_KERNEL_BUTTERFLY_RTC) {
     void* args[] = {&a};
@@ -1487,6 +1495,36 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   }
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
   HIP_CHECK(hipGetLastError());
+  return CVD_OK;
+}
+
+// Models [i0, i1) of a cvd_detect_multi call in one launch of the specialised kernel's
+// multi-model entry (k1b_multi, cvd_device.h); the caller checked they share it.
+static int launch_multi(const cvd_model* const* models, int32_t i0, int32_t i1, const uint32_t* const* d_r,
+                        int64_t N, const int64_t* nseq, const int64_t* n_h1, double* const* d_sums,
+                        int64_t* const* d_counts, void* stream, bool early) {
+  const cvd_model& M0 = *models[i0];
+  MultiArgs ma;
+  ma.nm = 0;
+  uint32_t blocks = 0;
+  const unsigned blk = (unsigned)M0.rtc_block;
+  for (int32_t i = i0; i < i1; ++i) {
+    const cvd_model& M = *models[i];
+    if (nseq[i] <= 0) continue;
+    const int64_t nb = (nseq[i] + blk - 1) / blk;
+    if ((int64_t)blocks + nb > (int64_t)UINT32_MAX) { set_error("multi-model launch: grid too large"); return CVD_E_INVALID; }
+    ma.a[ma.nm] = exp_args(M, CVD_KERNEL_BUTTERFLY_RTC, d_r[i], N, nseq[i], n_h1[i], d_sums ? d_sums[i] : nullptr,
+                           d_counts[i], nullptr, M.d_bfly, early);
+    blocks += (uint32_t)nb;
+    ma.blk_end[ma.nm] = blocks;
+    ++ma.nm;
+  }
+  if (ma.nm == 0) return CVD_OK;
+  for (int j = ma.nm; j < kMultiMax; ++j) ma.blk_end[j] = blocks;
+  void* args[] = {&ma};
+  const unsigned lds = M0.rtc_ldsf ? (unsigned)(M0.fcap * sizeof(uint32_t)) : 0u;
+  HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M0.rtc_fn_multi, blocks, 1, 1, blk, 1, 1, lds, (hipStream_t)stream,
+                                  args, nullptr));
   return CVD_OK;
 }
 
@@ -1519,6 +1557,8 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
     if ((rc = dev_copy(M.d_bfly, M.bfly))) return rc;
   }
+  HIP_CHECK(hipMalloc((void**)&M.d_err, sizeof(int32_t)));
+  HIP_CHECK(hipMemset(M.d_err, 0, sizeof(int32_t)));
   M.device = device;
   // smallest per-step log P̂1 (early decision bound): every row entry and, for
   // sparse models, the unvisited-row value
@@ -1528,6 +1568,7 @@ int cvd::upload_model(cvd_model& M, int device) {
   // table-driven kernel runs (same results), and the reason is kept for
   // cvd_model_jit_status
   M.rtc_fn = nullptr;
+  M.rtc_fn_multi = nullptr;
   M.jit_error.clear();
   M.rtc_ldsf = M.k1b_ok && M.hcap > 0 && ldsf_preferred(M);
   // block size: 512 threads with the LDS filter (two blocks of 8 waves per CU hold it),
@@ -1536,8 +1577,10 @@ int cvd::upload_model(cvd_model& M, int device) {
   if (M.rtc_block != 256 && M.rtc_block != 512 && M.rtc_block != 1024) M.rtc_block = kBlock;
   const std::string vdefs = "-DCVD_K1B_BLOCK=" + std::to_string(M.rtc_block) +
                             (M.rtc_ldsf ? " -DCVD_K1B_LDSF=1 -DCVD_FILTER_PAT_BITS=" + std::to_string(kFilterPatBitsLds) : "");
-  if (M.k1b_ok && M.hcap > 0 && rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn) != 0) {
+  if (M.k1b_ok && M.hcap > 0 &&
+      rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn, &M.rtc_fn_multi) != 0) {
     M.rtc_fn = nullptr;
+    M.rtc_fn_multi = nullptr;
     M.rtc_ldsf = false;
     M.rtc_block = kBlock;
     M.jit_error = last_error_copy();
@@ -1551,7 +1594,7 @@ void cvd::free_model_device(cvd_model& M) {
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
   void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_filt_lds, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
-                  M.d_bmk1, M.d_bfly};
+                  M.d_bmk1, M.d_bfly, M.d_err};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
@@ -1559,7 +1602,9 @@ void cvd::free_model_device(cvd_model& M) {
   M.d_bmp = nullptr;
   M.d_bmk1 = nullptr;
   M.d_bfly = nullptr;
+  M.d_err = nullptr;
   M.rtc_fn = nullptr;
+  M.rtc_fn_multi = nullptr;
   M.device = -1;
   (void)hipSetDevice(cur);
 }
@@ -1632,6 +1677,58 @@ extern "C" int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N
   return CVD_E_INVALID;
 }
 
+// Models i and j can share one multi-model launch: the same specialised kernel variant
+// (decoder code, block size, LDS filter) on the same device, explicit best path.
+static bool multi_ok(const cvd_model& M) {
+  return M.kind == 1 && M.rtc_fn && M.rtc_fn_multi && !std::getenv("CVD_NO_MULTI");
+}
+static bool multi_same(const cvd_model& A, const cvd_model& B) {
+  return A.rtc_fn_multi == B.rtc_fn_multi && A.rtc_block == B.rtc_block && A.rtc_ldsf == B.rtc_ldsf &&
+         A.device == B.device && (!A.rtc_ldsf || A.fcap == B.fcap);
+}
+
+extern "C" int cvd_detect_multi(const cvd_model* const* models, int32_t nm, const uint32_t* const* d_r, int64_t N,
+                                const int64_t* nseq, const int64_t* n_h1, double* const* d_sums,
+                                int64_t* const* d_counts, int32_t path, void* stream) {
+  if (!models || nm < 0 || (nm > 0 && (!d_r || !nseq || !n_h1 || !d_counts)) || N < 0) {
+    set_error("bad detect_multi arguments");
+    return CVD_E_INVALID;
+  }
+  const bool early = (path & CVD_DETECT_EARLY_DECISION) != 0;
+  const int32_t base = path & ~CVD_DETECT_EARLY_DECISION;
+  for (int32_t i = 0; i < nm; ++i) {
+    if (!models[i] || (!d_r[i] && N > 0 && nseq[i] > 0) || !d_counts[i] || nseq[i] < 0 || n_h1[i] < 0 ||
+        n_h1[i] > nseq[i]) {
+      set_error("bad detect_multi arguments");
+      return CVD_E_INVALID;
+    }
+    if (early && d_sums && d_sums[i]) {
+      set_error("early decision stops a trial once its decision is certain: per-trial sums need the full run");
+      return CVD_E_INVALID;
+    }
+    const int rc = check_device(*models[i]);
+    if (rc) return rc;
+  }
+  int32_t i = 0;
+  while (i < nm) {
+    const cvd_model& M = *models[i];
+    const bool mok = (base == CVD_PATH_AUTO || base == CVD_PATH_EXPLICIT) && multi_ok(M);
+    int32_t j = i + 1;
+    if (mok)
+      while (j < nm && j - i < kMultiMax && multi_ok(*models[j]) && multi_same(M, *models[j])) ++j;
+    int rc;
+    if (mok && j - i > 1) {
+      rc = launch_multi(models, i, j, d_r, N, nseq, n_h1, d_sums, d_counts, stream, early);
+    } else {
+      j = i + 1;
+      rc = cvd_detect(models[i], d_r[i], N, nseq[i], n_h1[i], d_sums ? d_sums[i] : nullptr, d_counts[i], path, stream);
+    }
+    if (rc) return rc;
+    i = j;
+  }
+  return CVD_OK;
+}
+
 extern "C" int cvd_trace(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
                          uint8_t* d_D, void* stream) {
   if (!model || (!d_r && N > 0 && nseq > 0) || (!d_D && nseq > 0) || N < 0 || nseq < 0) {
@@ -1656,10 +1753,38 @@ extern "C" int64_t cvd_mc_workspace_bytes(const cvd_code* enc1, int64_t N, int64
   return w4 * 4 * 2 * batch * (int64_t)sizeof(uint32_t);
 }
 
+// Trials per launch of the fused kernel: its grid has 2 Tp lanes (HIP bounds a grid at
+// 2^32 work-items), so cvd_mc_run and cvd_mc_fused slice longer ranges; a slice of 2^28
+// trials is ~2,000 residency rounds, so the slicing costs nothing measurable.
+// CVD_MC_FUSED_SLICE lowers it (tests run the multi-slice path with small ranges).
+static int64_t fused_slice() {
+  const char* e = std::getenv("CVD_MC_FUSED_SLICE");
+  const int64_t v = e && *e ? std::atoll(e) : 0;
+  return v > 0 ? std::min<int64_t>(v, (int64_t)1 << 28) : ((int64_t)1 << 28);
+}
+
+static int mc_fused_sliced(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint64_t seed, uint32_t tag,
+                           uint64_t thr, int64_t N, int64_t trial_begin, int64_t trial_end, double* d_sums,
+                           int64_t* d_counts, void* stream, bool early) {
+  const int64_t sl = fused_slice();
+  for (int64_t b = trial_begin; b < trial_end; b += sl) {
+    const int64_t T = std::min(sl, trial_end - b);
+    const int rc = launch_mc_fused(M, e1, e2, (uint32_t)seed, (uint32_t)(seed >> 32), tag, thr, N, b, T,
+                                   d_sums ? d_sums + 4 * (b - trial_begin) : nullptr, d_counts, stream, early);
+    if (rc) return rc;
+  }
+  return CVD_OK;
+}
+
+// Whether cvd_mc_run (path, model) runs the fused kernel and so needs no workspace.
+static bool mc_run_fused(const cvd_model& M, int32_t path) {
+  return (path & ~CVD_DETECT_EARLY_DECISION) == CVD_PATH_AUTO && mc_fused_preferred(M);
+}
+
 extern "C" int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2,
                           double p, int64_t N, uint64_t seed, int64_t trial_begin, int64_t trial_end,
                           int64_t batch, void* d_work, int64_t* d_counts, int32_t path, void* stream) {
-  if (!model || !d_work || !d_counts || trial_end < trial_begin || batch <= 0 || N < 0) {
+  if (!model || !d_counts || trial_end < trial_begin || batch <= 0 || N < 0) {
     set_error("bad mc_run arguments");
     return CVD_E_INVALID;
   }
@@ -1674,12 +1799,17 @@ extern "C" int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cv
   const uint32_t tag = grid_tag(N, p);
   const uint64_t thr = noise_threshold(p);
   const bool early = (path & CVD_DETECT_EARLY_DECISION) != 0;
-  if ((path & ~CVD_DETECT_EARLY_DECISION) == CVD_PATH_AUTO && mc_fused_preferred(*model)) {
-    // LDS-resident dense models: the fused trial kernel, no streams in HBM (same counts)
+  if (mc_run_fused(*model, path)) {
+    // LDS-resident dense models: the fused trial kernel, no streams in HBM (same counts),
+    // in slices of at most fused_slice() trials per launch
     if ((rc = check_device(*model))) return rc;
-    rc = launch_mc_fused(*model, e1, e2, (uint32_t)seed, (uint32_t)(seed >> 32), tag, thr, N, trial_begin,
-                         trial_end - trial_begin, nullptr, d_counts, stream, early);
+    rc = mc_fused_sliced(*model, e1, e2, seed, tag, thr, N, trial_begin, trial_end, nullptr, d_counts, stream,
+                         early);
     if (rc != CVD_E_UNSUPPORTED) return rc;
+  }
+  if (!d_work) {
+    set_error("cvd_mc_run: this model and path need the stream workspace (cvd_mc_workspace_bytes)");
+    return CVD_E_INVALID;
   }
   uint32_t* r = static_cast<uint32_t*>(d_work);
   for (int64_t b = trial_begin; b < trial_end; b += batch) {
@@ -1712,6 +1842,67 @@ extern "C" int cvd_mc_fused(const cvd_model* model, const cvd_code* enc1, const 
     return CVD_E_INVALID;
   }
   if ((rc = check_device(*model))) return rc;
-  return launch_mc_fused(*model, e1, e2, (uint32_t)seed, (uint32_t)(seed >> 32), grid_tag(N, p), noise_threshold(p),
-                         N, trial_begin, trial_end - trial_begin, d_sums, d_counts, stream, early);
+  return mc_fused_sliced(*model, e1, e2, seed, grid_tag(N, p), noise_threshold(p), N, trial_begin, trial_end, d_sums,
+                         d_counts, stream, early);
+}
+
+extern "C" int cvd_model_device_error(cvd_model* model, int32_t* flags_out) {
+  if (!model || !flags_out) { set_error("null argument"); return CVD_E_INVALID; }
+  *flags_out = 0;
+  if (model->device < 0 || !model->d_err) return CVD_OK;
+  int cur = 0;
+  HIP_CHECK(hipGetDevice(&cur));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{cur};
+  HIP_CHECK(hipSetDevice(model->device));
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(flags_out, model->d_err, sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemset(model->d_err, 0, sizeof(int32_t)));
+  if (*flags_out) {
+    set_error("detector kernel error flags set (bit 0: walk-mode scheduler guard hit; the launch's counts are void)");
+    return CVD_E_STATE;
+  }
+  return CVD_OK;
+}
+
+// ─────────────── the (N, p) grid in one call ───────────────
+
+extern "C" int64_t cvd_mc_grid_workspace_bytes(const cvd_model* const* models, int32_t np, const cvd_code* enc1,
+                                               const int64_t* N, int32_t nN, int64_t batch, int32_t path) {
+  if (!models || np <= 0 || !enc1 || !N || nN <= 0 || batch <= 0) return -1;
+  bool need = false;
+  for (int32_t i = 0; i < np; ++i) {
+    if (!models[i]) return -1;
+    need = need || !mc_run_fused(*models[i], path);
+  }
+  if (!need) return 0;   // every point runs the fused kernel
+  int64_t best = 0;
+  for (int32_t j = 0; j < nN; ++j) {
+    if (N[j] < 0) return -1;
+    best = std::max(best, cvd_mc_workspace_bytes(enc1, N[j], batch));
+  }
+  return best;
+}
+
+extern "C" int cvd_mc_run_grid(const cvd_model* const* models, const cvd_code* enc1, const cvd_code* enc2,
+                               const double* p, int32_t np, const int64_t* N, int32_t nN, uint64_t seed,
+                               int64_t trial_begin, int64_t trial_end, int64_t batch, void* d_work,
+                               int64_t* d_counts, int32_t path, void* stream) {
+  if (!models || !p || !N || np <= 0 || nN <= 0 || !d_counts) {
+    set_error("bad mc_run_grid arguments");
+    return CVD_E_INVALID;
+  }
+  for (int32_t i = 0; i < np; ++i)
+    if (!models[i]) { set_error("mc_run_grid: null model"); return CVD_E_INVALID; }
+  // Pd_plotter.py:196-233: N outer, p inner, num_iter trials at every point; the point
+  // (N[j], p[i]) accumulates into d_counts[(j * np + i) * 2 .. + 1]
+  for (int32_t j = 0; j < nN; ++j)
+    for (int32_t i = 0; i < np; ++i) {
+      const int rc = cvd_mc_run(models[i], enc1, enc2, p[i], N[j], seed, trial_begin, trial_end, batch, d_work,
+                                d_counts + 2 * ((int64_t)j * np + i), path, stream);
+      if (rc) return rc;
+    }
+  return CVD_OK;
 }

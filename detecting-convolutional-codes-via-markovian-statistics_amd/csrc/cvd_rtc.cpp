@@ -49,7 +49,7 @@ extern char** environ;
 namespace {
 
 std::mutex g_mu;
-std::map<std::tuple<int, int, uint64_t, std::string>, hipFunction_t> g_cache;
+std::map<std::tuple<int, int, uint64_t, std::string>, std::pair<hipFunction_t, hipFunction_t>> g_cache;
 
 uint64_t fnv1a(const std::string& s, uint64_t h = 0xcbf29ce484222325ull) {
   for (unsigned char c : s) { h ^= c; h *= 0x100000001b3ull; }
@@ -94,12 +94,15 @@ const char* kClangFlags[] = {"-O3", "-std=c++17", "-ffp-contract=off",
                              // interleaved A/B (profiles/r01g_ab/), same registers, no spills
                              "-mllvm", "--amdgpu-sched-strategy=max-ilp"};
 
+// two entries per code: one model per launch, and several (k1b_multi, cvd_detect_multi)
 std::string entry_source(int m, uint64_t xm) {
-  char entry[256];
+  char entry[640];
   std::snprintf(entry, sizeof(entry),
                 "\nextern \"C\" __global__ __launch_bounds__(cvd_dev::kK1bBlock, cvd_dev::kK1bWavesPerSimd)\n"
-                "void cvd_k1b_spec(cvd_dev::ExpArgs a) { cvd_dev::k1b_body<%d, true, 0x%016llxull, false>(a); }\n",
-                m, (unsigned long long)xm);
+                "void cvd_k1b_spec(cvd_dev::ExpArgs a) { cvd_dev::k1b_body<%d, true, 0x%016llxull, false>(a, blockIdx.x); }\n"
+                "extern \"C\" __global__ __launch_bounds__(cvd_dev::kK1bBlock, cvd_dev::kK1bWavesPerSimd)\n"
+                "void cvd_k1b_spec_multi(cvd_dev::MultiArgs a) { cvd_dev::k1b_multi<%d, 0x%016llxull>(a); }\n",
+                m, (unsigned long long)xm, m, (unsigned long long)xm);
   return entry;
 }
 
@@ -218,9 +221,12 @@ bool compile_hiprtc(const std::string& src0, const std::string& arch, const std:
 
 }  // namespace
 
-// hipFunction_t of cvd_k1b_spec<m, code> on `device`, compiling it on first use.
-int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, void** fn_out) {
+// hipFunction_t of cvd_k1b_spec<m, code> (and of its multi-model entry
+// cvd_k1b_spec_multi, same module) on `device`, compiling them on first use.
+int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, void** fn_out,
+                          void** fn_multi_out) {
   *fn_out = nullptr;
+  if (fn_multi_out) *fn_multi_out = nullptr;
   if (const char* e = std::getenv("CVD_NO_JIT"))
     if (e[0] && e[0] != '0') { set_error("JIT: disabled by CVD_NO_JIT"); return -1; }
   std::lock_guard<std::mutex> lock(g_mu);
@@ -241,7 +247,8 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
   const auto key = std::make_tuple(device, m, xm, all_defs);
   auto it = g_cache.find(key);
   if (it != g_cache.end()) {
-    *fn_out = (void*)it->second;
+    *fn_out = (void*)it->second.first;
+    if (fn_multi_out) *fn_multi_out = (void*)it->second.second;
     return 0;
   }
   hipDeviceProp_t prop;
@@ -267,31 +274,32 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
       cpath = dir + name;
     }
   }
-  auto load = [&](hipFunction_t& fn) {
+  auto load = [&](hipFunction_t& fn, hipFunction_t& fnm) {
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(device);
     hipModule_t mod;
     const bool loaded = hipModuleLoadData(&mod, code.data()) == hipSuccess &&
-                        hipModuleGetFunction(&fn, mod, "cvd_k1b_spec") == hipSuccess;
+                        hipModuleGetFunction(&fn, mod, "cvd_k1b_spec") == hipSuccess &&
+                        hipModuleGetFunction(&fnm, mod, "cvd_k1b_spec_multi") == hipSuccess;
     (void)hipSetDevice(cur);
     return loaded;
   };
-  hipFunction_t fn;
+  hipFunction_t fn, fnm;
+  auto done = [&]() {
+    g_cache[key] = std::make_pair(fn, fnm);   // modules live for the process (one per device and code)
+    *fn_out = (void*)fn;
+    if (fn_multi_out) *fn_multi_out = (void*)fnm;
+    return 0;
+  };
   if (!cpath.empty() && cache_load(cpath, code)) {
-    if (load(fn)) {
-      g_cache[key] = fn;
-      *fn_out = (void*)fn;
-      return 0;
-    }
+    if (load(fn, fnm)) return done();
     ::unlink(cpath.c_str());   // unusable cached object: rebuild it
   }
   bool ok = !force_rtc && compile_clang(src, arch, all_defs, code, err1);
   if (ok && !cpath.empty()) cache_store(cpath, code);
   if (!ok) ok = compile_hiprtc(src, arch, all_defs, code, err2);
   if (!ok) { set_error("JIT: " + err1 + " | " + err2); return -1; }
-  if (!load(fn)) { set_error("JIT: module load failed"); return -1; }
-  g_cache[key] = fn;   // modules live for the process (one per device and code)
-  *fn_out = (void*)fn;
-  return 0;
+  if (!load(fn, fnm)) { set_error("JIT: module load failed"); return -1; }
+  return done();
 }

@@ -193,6 +193,13 @@ class Model:
                           f"butterfly kernel (same results, slower): {msg}", RuntimeWarning, stacklevel=2)
         return self
 
+    def device_error(self):
+        """Raise if a launch on this model set a kernel error flag since the last check
+        (cvd_model_device_error: walk mode's scheduler guard; synchronises the device)."""
+        flags = ctypes.c_int32()
+        _lib.check(self._lib.cvd_model_device_error(self._h, ctypes.byref(flags)))
+        return int(flags.value)
+
     def jit_status(self):
         """(1 built | -1 unavailable | 0 not applicable, reason) of the code-specialised kernel."""
         buf = ctypes.create_string_buffer(4096)
@@ -298,6 +305,44 @@ class Detector:
                                          _stream_ptr(stream)))
         return counts
 
+    def detect_multi(self, models, bufs, N, nseq, n_h1, counts, sums=None, path=_lib.PATH_AUTO, stream=None,
+                     early_decision=False):
+        """len(models) detect() calls in as few launches as possible (cvd_detect_multi):
+        model i over stream buffer bufs[i] (nseq[i] sequences, the first n_h1[i] H1),
+        accumulating counts[i] (and sums[i] if given); models that share the specialised
+        kernel variant run in one launch, so a p sweep pays one last-round tail."""
+        k = len(models)
+        if not (len(bufs) == len(nseq) == len(n_h1) == len(counts) == k) or (sums is not None and len(sums) != k):
+            raise ValueError("one buffer, nseq, n_h1 and counts entry per model")
+        if early_decision:
+            path = int(path) | _lib.DETECT_EARLY_DECISION
+        P = ctypes.c_void_p * max(k, 1)
+        hs = P(*[m.handle.value for m in models])
+        rs = P(*[r.data_ptr() for r in bufs])
+        cs = P(*[c.data_ptr() for c in counts])
+        ss = P(*[(x.data_ptr() if x is not None else 0) for x in sums]) if sums is not None else None
+        nv = (ctypes.c_int64 * max(k, 1))(*[int(x) for x in nseq])
+        hv = (ctypes.c_int64 * max(k, 1))(*[int(x) for x in n_h1])
+        _lib.check(_lib.lib().cvd_detect_multi(hs, k, rs, int(N), nv, hv, ss, cs, int(path), _stream_ptr(stream)))
+        return counts
+
+    @staticmethod
+    def multi_groups(models):
+        """Index runs of `models` that cvd_detect_multi merges into one launch (the same
+        specialised kernel variant; at most 8 per launch) -- for per-launch timing."""
+        groups, cur, key = [], [], None
+        for i, m in enumerate(models):
+            inf = m.info()
+            k = (inf["explicit_kernel"], inf["lds_filter"]) if inf["kind"] == 1 and inf["explicit_kernel"] == 4 else None
+            if cur and (k is None or k != key or len(cur) == 8 or os.environ.get("CVD_NO_MULTI")):
+                groups.append(cur)
+                cur = []
+            cur.append(i)
+            key = k
+        if cur:
+            groups.append(cur)
+        return groups
+
     def trace(self, model, r, N, nseq, stream=None):
         """D_0..D_N of every sequence on the explicit path: uint8 [N+1, nseq, 2^m]."""
         D = torch.empty((int(N) + 1, int(nseq), 1 << self.m), dtype=torch.uint8, device=self.device)
@@ -353,12 +398,16 @@ class Detector:
         batch = self.default_batch(N, T) if batch is None else int(batch)
         lib = _lib.lib()
         if not return_sums:
-            wsz = lib.cvd_mc_workspace_bytes(g1.c, int(N), batch)
-            work = torch.empty(max(wsz, 4) // 4, dtype=torch.int32, device=self.device)
+            # the fused kernel (PATH_AUTO on an mc_fused model) needs no stream workspace
+            fused_auto = int(path) == _lib.PATH_AUTO and bool(model.info()["mc_fused"])
+            work = None
+            if not fused_auto:
+                wsz = lib.cvd_mc_workspace_bytes(g1.c, int(N), batch)
+                work = torch.empty(max(wsz, 4) // 4, dtype=torch.int32, device=self.device)
             flags = _lib.DETECT_EARLY_DECISION if early_decision else 0
             _lib.check(lib.cvd_mc_run(model.handle, g1.c, g2.c, float(p), int(N),
                                       int(seed) & 0xFFFFFFFFFFFFFFFF, int(trial_begin), int(trial_end),
-                                      batch, ctypes.c_void_p(work.data_ptr()),
+                                      batch, ctypes.c_void_p(work.data_ptr() if work is not None else 0),
                                       ctypes.c_void_p(counts.data_ptr()), int(path) | flags, _stream_ptr(stream)))
             return {"counts": counts}
         tag = grid_tag(N, p)
@@ -373,6 +422,38 @@ class Detector:
             s = sums.cpu().numpy()
             out.append(np.concatenate([s[:Tb], s[Tb:]], axis=1))
         return {"counts": counts, "sums": np.concatenate(out, axis=0)}
+
+
+    def run_grid(self, models, gen1, gen2, p_list, N_list, seed, trial_begin, trial_end, batch=None,
+                 path=_lib.PATH_AUTO, counts=None, stream=None, early_decision=False):
+        """The (N, p) grid of Pd_plotter.py:196-233 in ONE library call (cvd_mc_run_grid,
+        SURVEY.md §8(b)): models[i] learned at p_list[i]; global trials [trial_begin,
+        trial_end) at every point; returns the int64 counts [len(N_list), len(p_list), 2]."""
+        g1 = as_code(gen1, self.m, self.k, self.n)
+        g2 = as_code(gen2, self.m, self.k, self.n)
+        npn, nN = len(p_list), len(N_list)
+        if len(models) != npn:
+            raise ValueError("one model per p")
+        if counts is None:
+            counts = torch.zeros((nN, npn, 2), dtype=torch.int64, device=self.device)
+        T = int(trial_end) - int(trial_begin)
+        if T <= 0:
+            return counts
+        batch = self.default_batch(max(N_list), T) if batch is None else int(batch)
+        hs = (ctypes.c_void_p * npn)(*[m.handle.value for m in models])
+        pv = (ctypes.c_double * npn)(*[float(p) for p in p_list])
+        Nv = (ctypes.c_int64 * nN)(*[int(N) for N in N_list])
+        lib = _lib.lib()
+        flags = _lib.DETECT_EARLY_DECISION if early_decision else 0
+        wsz = lib.cvd_mc_grid_workspace_bytes(hs, npn, g1.c, Nv, nN, batch, int(path) | flags)
+        if wsz < 0:
+            raise _lib.CvdError("cvd_mc_grid_workspace_bytes: bad arguments")
+        work = torch.empty(max(wsz, 4) // 4, dtype=torch.int32, device=self.device) if wsz > 0 else None
+        _lib.check(lib.cvd_mc_run_grid(hs, g1.c, g2.c, pv, npn, Nv, nN, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                       int(trial_begin), int(trial_end), batch,
+                                       ctypes.c_void_p(work.data_ptr() if work is not None else 0),
+                                       ctypes.c_void_p(counts.data_ptr()), int(path) | flags, _stream_ptr(stream)))
+        return counts
 
 
 # ───────────────────── reference-mirroring functions ────────────────────────
@@ -467,6 +548,8 @@ def enumerate_states_device(generator_matrix, m, k, n, device=0, cap=1 << 40, me
     rc = lib.cvd_enumerate_device(code.c, int(device), int(cap), int(mem_bytes), ctypes.byref(S), None, None,
                                   lv.ctypes.data, int(max_levels), ctypes.byref(nl), None)
     if rc not in (0, -3):
+        _lib.check(rc)
+    if rc == -3 and S.value < 1:   # CVD_E_CAPACITY certifies S_out >= 1; anything else is a failure
         _lib.check(rc)
     out = {"S": int(S.value), "complete": rc == 0, "level_sizes": lv[:min(nl.value, max_levels)].tolist()}
     if with_tables and rc == 0:

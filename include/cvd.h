@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 7
+#define CVD_ABI_VERSION 8
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -209,6 +209,20 @@ int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int
 int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
                int64_t n_h1, double* d_sums, int64_t* d_counts, int32_t path, void* stream);
 
+/* nm cvd_detect calls in as few launches as possible (a p sweep: one model per p, one
+ * stream buffer each; Pd_plotter.py:199-233).  Model i reads d_r[i] (nseq[i] sequences,
+ * the first n_h1[i] of them H1) and accumulates d_counts[i][2] (and d_sums[i] when d_sums
+ * and d_sums[i] are non-NULL), all with the same N.  Consecutive models that share the
+ * code-specialised kernel variant (CVD_KERNEL_BUTTERFLY_RTC: same decoder, block size
+ * and filter placement) run in ONE launch, up to 8 per launch, block ranges in model
+ * order, so the step pays one last-round tail instead of one per model; others run as
+ * cvd_detect.  Results equal the separate calls exactly.  path: CVD_PATH_AUTO or
+ * CVD_PATH_EXPLICIT (merged), any other path launches one model at a time; OR
+ * CVD_DETECT_EARLY_DECISION as in cvd_detect.  CVD_NO_MULTI=1 disables merging. */
+int cvd_detect_multi(const cvd_model* const* models, int32_t nm, const uint32_t* const* d_r, int64_t N,
+                     const int64_t* nseq, const int64_t* n_h1, double* const* d_sums, int64_t* const* d_counts,
+                     int32_t path, void* stream);
+
 /* Metric trace on the explicit path: d_D[(t*nseq + q)*2^m + s] = D_t(s), t = 0..N. */
 int cvd_trace(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
               uint8_t* d_D, void* stream);
@@ -220,6 +234,31 @@ int64_t cvd_mc_workspace_bytes(const cvd_code* enc1, int64_t N, int64_t batch);
 int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc2,
                double p, int64_t N, uint64_t seed, int64_t trial_begin, int64_t trial_end,
                int64_t batch, void* d_work, int64_t* d_counts, int32_t path, void* stream);
+
+/* cvd_mc_run: d_work may be NULL when the call runs the fused kernel below (CVD_PATH_AUTO
+ * and cvd_model_info.mc_fused); otherwise it returns CVD_E_INVALID without it.  The fused
+ * path launches at most 2^28 trials per kernel (HIP grid limit), in slices. */
+
+/* The whole (N, p) grid of Pd_plotter.py:196-233 in one call: N outer,
+ * p inner, the global trials [trial_begin, trial_end) at every point (the reference's
+ * num_iter per point; a shard of them under trial sharding), with models[i] the model
+ * learned at p[i] (learn_P1_empirical is per p, Pd_plotter.py:123-169).  Point
+ * (N[j], p[i]) accumulates into d_counts[(j*np + i)*2 + {0: H1, 1: H2}] -- the
+ * [nN][np][2] count tensor cvd_allreduce_counts reduces -- exactly as np * nN
+ * cvd_mc_run calls would.  d_work: cvd_mc_grid_workspace_bytes (the largest N's
+ * workspace; 0 = NULL allowed when every point runs the fused kernel). */
+int64_t cvd_mc_grid_workspace_bytes(const cvd_model* const* models, int32_t np, const cvd_code* enc1,
+                                    const int64_t* N, int32_t nN, int64_t batch, int32_t path);
+int cvd_mc_run_grid(const cvd_model* const* models, const cvd_code* enc1, const cvd_code* enc2,
+                    const double* p, int32_t np, const int64_t* N, int32_t nN, uint64_t seed,
+                    int64_t trial_begin, int64_t trial_end, int64_t batch, void* d_work,
+                    int64_t* d_counts, int32_t path, void* stream);
+
+/* Kernel error flags of a model's launches since the last call (synchronises its
+ * device): bit 0 = a walk-mode wave (k1b_walk) left its scheduler loop by the guard
+ * bound with lanes unfinished, so that launch's counts and sums are void.  Returns
+ * CVD_E_STATE when any flag is set (then cleared), CVD_OK otherwise. */
+int cvd_model_device_error(cvd_model* model, int32_t* flags_out);
 
 /* The same grid point in ONE kernel per launch, without streams in HBM: every lane
  * generates its own sequence's received words (cvd_generate's encoder and noise, bit

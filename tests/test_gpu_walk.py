@@ -38,6 +38,7 @@ def test_walk_equals_lockstep(pkg, monkeypatch, p):
         got, gc = _sums(det, model, cc, N, p, t0, t1)
         assert np.array_equal(got, ref), (p, N)
         assert gc == rc
+    assert model.device_error() == 0      # no walk wave left its loop by the guard
 
 
 @pytest.mark.parametrize("wmin,amin,burst", [("1", "64", "1"), ("64", "1", "3"), ("8", "16", "64")])
@@ -149,10 +150,11 @@ def test_lds_filter_model_under_jit_fallbacks(pkg, monkeypatch, how):
         warnings.simplefilter("ignore", RuntimeWarning)
         alt = pkg.Model(det.dec, p, 300_000, 200, 1.0, SEED).upload(0)
     inf = alt.info()
+    # info.walk reports what runs: walk mode needs the specialised kernel
     if how == "hiprtc":
-        assert inf["explicit_kernel"] == 4 and inf["lds_filter"] == 1
+        assert inf["explicit_kernel"] == 4 and inf["lds_filter"] == 1 and inf["walk"] == 1
     else:
-        assert inf["explicit_kernel"] == 3 and inf["lds_filter"] == 0
+        assert inf["explicit_kernel"] == 3 and inf["lds_filter"] == 0 and inf["walk"] == 0
     got, gc = _sums(det, alt, cc, N, p, t0, t1)
     assert np.array_equal(got, ref)
     assert gc == rc
