@@ -89,6 +89,13 @@ def parse():
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None,
                     help="trials per GPU per p per step (a step runs every p of the config's grid)")
+    ap.add_argument("--sweep", default="per-p", choices=["per-p", "all"],
+                    help="per-p: a step is one batch at one p (step s at p_grid[s %% #p]) and value weighs "
+                         "every p equally from the per-p mean step times; all: a step is one batch at every p "
+                         "(multi-model launches), value = trials / elapsed")
+    ap.add_argument("--group-streams", type=int, default=1,
+                    help="device queues the step's detector launch groups are spread over (2: the LDS-filter "
+                         "model's launch beside the multi-model launch, so its last round is not a tail)")
     ap.add_argument("--multi", type=int, default=1,
                     help="detect a step's grid points in multi-model launches (cvd_detect_multi: the models "
                          "that share the specialised kernel variant in ONE launch, so the step pays one "
@@ -196,15 +203,22 @@ def main():
         models = dict(zip(p_grid, det.prepare_models(p_grid, a.learn_len if m == 6 else None, 200, 1.0, a.seed)))
         info = models[p_grid[0]].info()
     t_setup = time.perf_counter() - t_setup
-    # One step = one pass over the config's whole p grid (Pd_plotter.py:199-233 runs num_iter
-    # trials at every p): B trials per GPU at EVERY p, so the sweep's p are weighted equally
-    # whatever --steps is.  Whole residency rounds per launch: 4 waves/SIMD x 1024 SIMDs x 64
-    # lanes = 262,144 sequences (131,072 trials) per round.  m6: 3 rounds per p (2,359,296
-    # trials and 118 GB of streams per step); the six detector launches of a step run on
-    # --streams device queues, so one launch's last-round tail is filled by the next
-    # launch's waves (DESIGN.md "Measurement").  m2: 2^22 trials (one p); r23_m4: 2^17 per p.
-    B = a.batch or {"m6": 393_216, "m2": 4_194_304, "r23_m4": 131_072}[a.config]
+    # Steps and the weighting of the p grid (Pd_plotter.py:199-233 runs num_iter trials at
+    # EVERY p, so a sweep's throughput is (trials per p x #p) / sum over p of its time: the
+    # p weigh equally).
+    #  --sweep per-p (default): step s is one batch of B trials per GPU at p_grid[s % #p] --
+    #    C2's 1e7 trials per p run as launches of B = 2,621,440 trials (20 residency rounds
+    #    of 131,072 trials: 4 waves/SIMD x 1024 SIMDs x 64 lanes = 262,144 sequences; the
+    #    last round's uneven wave finish is < 1% of such a launch).  `value` = B x ranks /
+    #    (the mean over p of the mean step time at p), so every p weighs the same whatever
+    #    --steps is; `value_wall` = trials / elapsed of the same steps.
+    #  --sweep all: step s runs B trials at every p (the models that share the specialised
+    #    kernel variant in one launch, cvd_detect_multi); `value` = trials / elapsed.  The
+    #    smaller per-p batches cost ~2-3% against the per-p launches (profiles/r04c/).
+    sweep_all = a.sweep == "all"
     npg = len(p_grid)
+    B = a.batch or ({"m6": 655_360, "m2": 4_194_304, "r23_m4": 131_072} if sweep_all
+                    else {"m6": 2_621_440, "m2": 4_194_304, "r23_m4": 131_072})[a.config]
     if a.fused < 0:
         a.fused = int(not parity and bool(info["mc_fused"]))   # where it measured faster (cvd_model_info)
     if a.fused:
@@ -214,97 +228,136 @@ def main():
     buf_bytes = det.words_per_seq(N) * 4 * 2 * B
     if a.overlap and 2 * buf_bytes > (120 << 30):
         a.overlap = 0                          # two batches would not leave HBM headroom
-    # units: unit u of the run is grid point p_grid[u % npg] of step u // npg.  Overlap
-    # (table automaton): double-buffered generator on its own stream; otherwise one buffer
-    # per grid point, the step's generator launches first, then its detector launches --
-    # with --multi, the grid points whose models share the specialised kernel variant in
-    # one launch each (cvd_detect_multi; m6: p = 0.01 with its LDS filter, then the other
-    # five).  (Concurrent per-p launches on 2, 3 or 6 device queues measured 0.3%, 12% and
-    # 8% slower than one queue: the models' tables compete for the caches, profiles/r04a/.)
-    nbuf = 0 if a.fused else (2 if a.overlap else npg)
+    per_step = npg if sweep_all else 1        # grid points (launch units) per step
+
+    def units(s):
+        """the step's (grid point, first global trial id of this rank's batch)"""
+        tb = (s * world + rank) * B
+        return [(i, tb) for i in range(npg)] if sweep_all else [(s % npg, tb)]
+
+    # Overlap (table automaton): double-buffered generator on its own stream, units in
+    # sequence; otherwise one buffer per unit of a step, the step's generator launches
+    # first, then its detector launches -- with --sweep all and --multi, the grid points
+    # whose models share the specialised kernel variant in one launch each (m6: p = 0.01
+    # with its LDS filter, then the other five).  (Concurrent per-p launches on 2, 3 or 6
+    # device queues measured 0.3%, 12% and 8% slower than one queue: the models' tables
+    # compete for the caches, profiles/r04a/.)
+    nbuf = 0 if a.fused else (2 if a.overlap else per_step)
     bufs = [det.stream_buffer(N, 2 * B) for _ in range(nbuf)]
     counts = torch.zeros((npg, 2), dtype=torch.int64, device=det.device)
     main = torch.cuda.current_stream()
     gstream = torch.cuda.Stream(device=det.device) if a.overlap else main
-    use_multi = bool(a.multi) and not (a.overlap or a.fused or parity)
-    groups = det.multi_groups([models[p] for p in p_grid]) if use_multi else [[i] for i in range(npg)]
+    use_multi = sweep_all and bool(a.multi) and not (a.overlap or a.fused or parity)
+    groups = (det.multi_groups([models[p] for p in p_grid]) if use_multi
+              else [[j] for j in range(per_step)])      # positions within a step's units
+    nq = 1 if (a.overlap or not sweep_all) else max(1, min(a.group_streams, len(groups)))
+    queues = [main] + [torch.cuda.Stream(device=det.device) for _ in range(nq - 1)]
 
-    def gen(u, ev=None):
+    def gen(unit, buf, ev=None):
         if a.fused:
             return   # the fused kernel generates its own words (detect below)
-        s, i = divmod(u, npg)
+        i, tb = unit
         p = p_grid[i]
-        tb = (s * world + rank) * B            # global trial ids of this rank's batch at this p
         tag = pkg.grid_tag(N, p)
-        r = bufs[u % nbuf]
         if ev is not None:
             ev[0].record(gstream)
-        det.generate(g1, N, p, a.seed, tag, 2 * tb, 2, B, out=r, q0=0, pitch=2 * B, stream=gstream)
-        det.generate(g2, N, p, a.seed, tag, 2 * tb + 1, 2, B, out=r, q0=B, pitch=2 * B, stream=gstream)
+        det.generate(g1, N, p, a.seed, tag, 2 * tb, 2, B, out=buf, q0=0, pitch=2 * B, stream=gstream)
+        det.generate(g2, N, p, a.seed, tag, 2 * tb + 1, 2, B, out=buf, q0=B, pitch=2 * B, stream=gstream)
         if ev is not None:
             ev[1].record(gstream)
 
     early = [False]
 
-    def detect(u0, grp, st, ev=None):
-        """grid points grp (indices into p_grid) of the step starting at unit u0"""
+    def detect(us, bs, st, ev=None):
+        """units us (with their stream buffers bs) in one call"""
         if ev is not None:
             ev[0].record(st)
-        if len(grp) > 1:
-            det.detect_multi([models[p_grid[i]] for i in grp], [bufs[(u0 + i) % nbuf] for i in grp], N,
-                             [2 * B] * len(grp), [B] * len(grp), [counts[i] for i in grp], stream=st,
-                             early_decision=early[0])
+        if len(us) > 1:
+            det.detect_multi([models[p_grid[i]] for i, _ in us], bs, N, [2 * B] * len(us), [B] * len(us),
+                             [counts[i] for i, _ in us], stream=st, early_decision=early[0])
         else:
-            i = grp[0]
-            u = u0 + i
-            s = u // npg
+            (i, tb), = us
             p = p_grid[i]
             if parity:
-                pkg.parity_detect(bufs[u % nbuf], n, N, 2 * B, B, tpl, a.gamma, counts=counts[i], stream=st)
+                pkg.parity_detect(bs[0], n, N, 2 * B, B, tpl, a.gamma, counts=counts[i], stream=st)
             elif a.fused:
-                tb = (s * world + rank) * B
                 det.run_trials(models[p], cc["gen1"], cc["gen2"], N, p, a.seed, tb, tb + B,
                                counts=counts[i], stream=st, early_decision=early[0], fused=True)
             else:
-                det.detect(models[p], bufs[u % nbuf], N, 2 * B, B, counts=counts[i], stream=st,
-                           early_decision=early[0])
+                det.detect(models[p], bs[0], N, 2 * B, B, counts=counts[i], stream=st, early_decision=early[0])
         if ev is not None:
             ev[1].record(st)
 
-    def run(steps, base, gev=None, dev=None):
-        """steps whole sweeps from step `base`; gev[u] generator events per unit, dev[s][g]
-        detector events per launch group g of step s"""
+    def run(steps, base, ev=None):
+        """steps from step `base`; ev: {"gen": per unit, "det": [step][group], "end": per step
+        (main stream, after the step's detector launches), "t0": start}"""
         if steps <= 0:
             return
-        u0 = base * npg
-        nu = steps * npg
+        if ev is not None:
+            ev["t0"].record(main)
         if not a.overlap:
             for s in range(steps):
-                for i in range(npg):
-                    gen(u0 + s * npg + i, gev[s * npg + i] if gev else None)
-                for g, grp in enumerate(groups):
-                    detect(u0 + s * npg, grp, main, dev[s][g] if dev else None)
+                us = units(base + s)
+                for j, u in enumerate(us):
+                    gen(u, bufs[j] if nbuf else None, ev["gen"][s * per_step + j] if ev else None)
+                if nq > 1:
+                    ready = torch.cuda.Event()
+                    ready.record(main)
+                    for q in queues[1:]:
+                        q.wait_event(ready)
+                # (nq > 1: the largest group goes last on the main queue, the others first on
+                # their own queues, so their last rounds overlap the large launch)
+                order = sorted(range(len(groups)), key=lambda g: len(groups[g])) if nq > 1 else range(len(groups))
+                for k, g in enumerate(order):
+                    q = queues[(len(groups) - 1 - k) % nq] if nq > 1 else main
+                    detect([us[j] for j in groups[g]], [bufs[j] for j in groups[g]] if nbuf else [None],
+                           q, ev["det"][s][g] if ev else None)
+                for q in queues[1:]:
+                    main.wait_stream(q)
+                if ev is not None:
+                    ev["end"][s].record(main)
             return
+        flat = [(s, j, u) for s in range(steps) for j, u in enumerate(units(base + s))]
+        nu = len(flat)
         done = [torch.cuda.Event() for _ in range(nu)]
         ready = [torch.cuda.Event() for _ in range(nu)]
-        gen(u0, gev[0] if gev else None)
+        gen(flat[0][2], bufs[0], ev["gen"][0] if ev else None)
         ready[0].record(gstream)
-        for u in range(nu):
-            main.wait_event(ready[u])
-            s, i = divmod(u, npg)
-            detect(u0 + s * npg, [i], main, dev[s][i] if dev else None)
-            done[u].record(main)
-            if u + 1 < nu:
-                if u >= 1:
-                    gstream.wait_event(done[u - 1])   # buffer (u+1)%2 was read by detect(u-1)
-                gen(u0 + u + 1, gev[u + 1] if gev else None)
-                ready[u + 1].record(gstream)
+        for x in range(nu):
+            s, j, u = flat[x]
+            main.wait_event(ready[x])
+            detect([u], [bufs[x % 2]], main, ev["det"][s][j] if ev else None)
+            done[x].record(main)
+            if ev is not None and j == per_step - 1:
+                ev["end"][s].record(main)
+            if x + 1 < nu:
+                if x >= 1:
+                    gstream.wait_event(done[x - 1])   # buffer (x+1)%2 was read by detect(x-1)
+                gen(flat[x + 1][2], bufs[(x + 1) % 2], ev["gen"][x + 1] if ev else None)
+                ready[x + 1].record(gstream)
         main.wait_stream(gstream)
 
     def make_events(steps):
-        gev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps * npg)]
-        dev = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in groups] for _ in range(steps)]
-        return gev, dev
+        E = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
+        return {"t0": E(), "gen": [[E(), E()] for _ in range(steps * per_step)],
+                "det": [[[E(), E()] for _ in groups] for _ in range(steps)], "end": [E() for _ in range(steps)]}
+
+    def step_times(ev, steps):
+        """ms of each step on the main stream (from the previous step's end)"""
+        out, prev = [], ev["t0"]
+        for s in range(steps):
+            out.append(prev.elapsed_time(ev["end"][s]))
+            prev = ev["end"][s]
+        return out
+
+    def weighted_value(st_ms, steps):
+        """per-p mode: B x ranks / mean over the p of the mean step time at p; all: trials / time"""
+        if sweep_all:
+            return world * npg * B / (np.mean(st_ms) * 1e-3), list(range(npg))
+        by = {}
+        for s in range(steps):
+            by.setdefault(s % npg, []).append(st_ms[s])
+        return world * B / (np.mean([np.mean(v) for v in by.values()]) * 1e-3), sorted(by)
 
     # warmup steps use trial ids far from the timed ones (base 10,000 steps)
     run(a.warmup, 10_000)
@@ -313,9 +366,9 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    gev, dev = make_events(a.steps)
+    ev = make_events(a.steps)
     t0 = time.perf_counter()
-    run(a.steps, 0, gev, dev)
+    run(a.steps, 0, ev)
     if dist:
         dist.all_reduce(counts)                # the one collective: success counts over RCCL
     torch.cuda.synchronize()
@@ -325,23 +378,37 @@ def main():
     elapsed = time.perf_counter() - t0
     def max_over_ranks(x):
         # RCCL reduces device tensors only; gloo host tensors
-        t = torch.tensor([x], device=det.device if a.dist_backend == "nccl" else "cpu", dtype=torch.float64)
+        t = torch.tensor(x if isinstance(x, list) else [x], device=det.device if a.dist_backend == "nccl" else "cpu",
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return [float(v) for v in t.tolist()] if isinstance(x, list) else float(t[0])
 
+    st_ms = step_times(ev, a.steps)
     if dist:
         elapsed = max_over_ranks(elapsed)
+        st_ms = max_over_ranks(st_ms)          # each step's time: the slowest rank's
     for mdl in models.values():
         mdl.device_error()                     # raises if a detector launch flagged an error
-    gen_ms = 0.0 if a.fused else float(np.mean([e[0].elapsed_time(e[1]) for e in gev])) * npg
+    gen_ms = 0.0 if a.fused else float(np.mean([e[0].elapsed_time(e[1]) for e in ev["gen"]])) * per_step
     # detector launches: per launch group, mean over the steps (ms)
-    grp_ms = [float(np.mean([dev[s][g][0].elapsed_time(dev[s][g][1]) for s in range(a.steps)]))
-              for g in range(len(groups))]
-    phase_ms = float(np.sum(grp_ms))           # the step's detector launches, back to back on one queue
+    grp_all = [[ev["det"][s][g][0].elapsed_time(ev["det"][s][g][1]) for s in range(a.steps)]
+               for g in range(len(groups))]
+    grp_ms = [float(np.mean(x)) for x in grp_all]
+    phase_ms = float(np.sum(grp_ms)) if nq == 1 else float(np.mean(
+        [max(ev["gen"][(s + 1) * per_step - 1][1].elapsed_time(ev["det"][s][g][1]) for g in range(len(groups)))
+         for s in range(a.steps)]))
     # the dominant launch (the roofline's kernel): the group with the most grid points
     gdom = max(range(len(groups)), key=lambda g: (len(groups[g]), grp_ms[g]))
     det_ms = grp_ms[gdom]
-    det_by_group = [{"p": [p_grid[i] for i in groups[g]], "ms": grp_ms[g]} for g in range(len(groups))]
+    if sweep_all:
+        det_by = [{"p": [p_grid[i] for i in groups[g]], "ms": grp_ms[g]} for g in range(len(groups))]
+    else:
+        det_by = [{"p": [p_grid[i]], "ms": float(np.mean(grp_all[0][i::npg])), "launches": len(grp_all[0][i::npg])}
+                  for i in range(min(npg, a.steps))]
+        # one launch per step: the detector's launch time weighted like `value` (mean over p)
+        det_ms = phase_ms = float(np.mean([x["ms"] for x in det_by]))
+    steps_at = [len(range(i, a.steps, npg)) if not sweep_all else a.steps for i in range(npg)]
+    value, p_covered = weighted_value(st_ms, a.steps)
 
     # the same steps (same trial ids) with early decision: counts must be identical
     early_out = None
@@ -352,9 +419,9 @@ def main():
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
-        gev2, dev2 = make_events(a.steps)
+        ev2 = make_events(a.steps)
         t1 = time.perf_counter()
-        run(a.steps, 0, gev2, dev2)
+        run(a.steps, 0, ev2)
         if dist:
             dist.all_reduce(counts)
         torch.cuda.synchronize()
@@ -362,26 +429,32 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         el2 = time.perf_counter() - t1
+        st2 = step_times(ev2, a.steps)
         if dist:
             el2 = max_over_ranks(el2)
+            st2 = max_over_ranks(st2)
         early[0] = False
-        d2 = [float(np.mean([dev2[s][g][0].elapsed_time(dev2[s][g][1]) for s in range(a.steps)]))
-              for g in range(len(groups))]
-        early_out = {"value": a.steps * npg * B * world / el2, "unit": "trials/s", "ms_per_step": el2 / a.steps * 1e3,
-                     "detector_ms_by_launch": [{"p": [p_grid[i] for i in groups[g]], "ms": d2[g]}
-                                               for g in range(len(groups))],
+        early_out = {"value": weighted_value(st2, a.steps)[0], "value_wall": a.steps * per_step * B * world / el2,
+                     "unit": "trials/s", "ms_per_step": el2 / a.steps * 1e3,
                      "counts_equal_full_run": bool(torch.equal(counts, full_counts)),
                      "note": "counts only: each trial stops once its decision is certain (rigorous IEEE "
                              "bounds on the remaining increments, CVD_DETECT_EARLY_DECISION); the "
                              "headline value above runs every step of every trial"}
         counts.copy_(full_counts)
 
+    # per-rank setup (model learning on the GPU + the JIT compile of the specialised kernel,
+    # every rank at once): the multi-rank rehearsal's evidence, one entry per rank
+    setup_by_rank = [{"rank": rank, "setup_s": t_setup, "host": socket.gethostname(), "device": local}]
+    if dist:
+        lst = [None] * world
+        dist.all_gather_object(lst, setup_by_rank[0])
+        setup_by_rank = lst
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
-    trials = a.steps * npg * B * world
-    value = trials / elapsed
+    trials = a.steps * per_step * B * world
+    value_wall = trials / elapsed
     # roofline of the dominant kernel (detector): algorithmic bytes = the packed received
     # streams read once, 2 * ceil(N * n / 8) bytes per trial, per launch of
     # the dominant launch group (m6: the multi-model launch of five grid points), over that
@@ -434,8 +507,8 @@ def main():
         if ipws:
             # VALU roofline of the detector (its binding resource): wave-instructions
             # per launch from the counter pass, over this run's live launch time
-            winst = ipws * (2 * B * npg / 64) * N          # the step's detector launches
-            ach = winst / (phase_ms * 1e-3)
+            winst = ipws * (2 * B * len(groups[gdom]) / 64) * N    # the dominant launch
+            ach = winst / (det_ms * 1e-3)
             cpi = pmc.get("valu_cycles_per_inst")
             valu = {"insts_per_wave_step": ipws, "achieved": ach, "peak": VALU_PEAK_WINST,
                     "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WINST,
@@ -444,16 +517,18 @@ def main():
                     "cycles_per_inst": cpi,
                     "issue_cycle_weighted_frac": (ach * cpi / (1024 * SHADER_GHZ * 1e9)) if cpi else None,
                     "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU, opcode mix x "
-                              "profiles/valu_issue_cycles.json) + live HIP-event time of the detector phase"}
+                              "profiles/valu_issue_cycles.json) + live HIP-event time of the launch"}
     c = counts.cpu().numpy()
-    per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, a.steps * B * world),
-                      "Pc": float(c[i, 0] + c[i, 1]) / max(1, 2 * a.steps * B * world),
+    per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, steps_at[i] * B * world),
+                      "Pc": float(c[i, 0] + c[i, 1]) / max(1, 2 * steps_at[i] * B * world),
+                      "trials": steps_at[i] * B * world,
                       "h1_successes": int(c[i, 0]), "h2_successes": int(c[i, 1])}
              for i, p in enumerate(p_grid)}
     out = {
         "metric": (METRIC if a.config == "m6" and not parity
                    else f"MC trials/sec ({a.config}, N={N}{', parity-template baseline' if parity else ''})"),
         "value": value,
+        "value_wall": value_wall,
         "unit": "trials/s",
         "n_gpus": world,
         "steps": a.steps,
@@ -465,11 +540,17 @@ def main():
         "dtype": "u16x2 (metrics) + f64 (log-likelihood sums)",
         "data": "synthetic: Philox4x32-10 encoder inputs and BSC(p) flips (build spec), learned P̂1",
         "config": {"name": a.config, "detector": a.detector,
-                   "workload": f"{a.config} pair {cc['gen1']} vs {cc['gen2']}, N={N}, p-sweep {p_grid}, "
-                               f"every p in every step ({B} trials per p per GPU)", "N": N, "p_grid": p_grid,
-                   "p_weighting": "equal: each step runs the same trials per GPU at every p of the grid "
-                                  "(Pd_plotter.py:199-233 runs num_iter trials per p)",
-                   "trials_per_p_per_step_per_gpu": B, "trials_per_step_per_gpu": B * npg,
+                   "workload": (f"{a.config} pair {cc['gen1']} vs {cc['gen2']}, N={N}, p-sweep {p_grid}, "
+                                + (f"every p in every step ({B} trials per p per GPU)" if sweep_all else
+                                   f"one p per step ({B} trials per GPU, step s at p_grid[s % {npg}])")),
+                   "N": N, "p_grid": p_grid, "sweep": a.sweep,
+                   "p_weighting": ("equal: each step runs the same trials per GPU at every p of the grid; value = "
+                                   "trials / elapsed" if sweep_all else
+                                   "equal: value = B x GPUs / (mean over p of the mean step time at p), the sweep's "
+                                   "throughput at the same trials per p (Pd_plotter.py:199-233 runs num_iter trials "
+                                   "per p) whatever --steps is; value_wall = trials / elapsed weighs p by its step count"),
+                   "p_covered": [p_grid[i] for i in p_covered],
+                   "trials_per_p_per_step_per_gpu": B, "trials_per_step_per_gpu": B * per_step,
                    "k": k, "n": n, "m": m,
                    "model": info["kind"] and "sparse(learned)" or "dense",
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
@@ -489,13 +570,14 @@ def main():
                      "algorithmic_bytes_per_launch": alg_launch, "avg_launch_ms": det_ms,
                      "launch_grid_points": [p_grid[i] for i in groups[gdom]],
                      "detector_launches_per_step": len(groups), "detector_ms_per_step": phase_ms,
-                     "step_achieved": npg * alg_bytes / (phase_ms * 1e-3) / 1e9,
                      "valu": valu},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": phase_ms,
                        "overlap": bool(a.overlap), "fused": bool(a.fused), "model_setup_s": t_setup,
+                       "setup_by_rank": setup_by_rank,
                        "multi_model_launches": use_multi,
-                       "seq_steps_per_s_detector": 2 * B * npg * N / (phase_ms * 1e-3),
-                       "detector_ms_by_launch": det_by_group,
+                       "seq_steps_per_s_detector": 2 * B * per_step * N / (phase_ms * 1e-3),
+                       "step_ms": st_ms,
+                       "detector_ms_by_launch": det_by,
                        "generator_pmc": gen_pmc,
                        # walk mode of the m = 6 kernel per grid point (cvd_model_info.walk)
                        "walk_by_p": {str(p): int(models[p].info().get("walk", 0)) for p in p_grid} if models else None,

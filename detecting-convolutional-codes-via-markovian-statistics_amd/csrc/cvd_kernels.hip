@@ -1872,37 +1872,89 @@ extern "C" int cvd_model_device_error(cvd_model* model, int32_t* flags_out) {
 extern "C" int64_t cvd_mc_grid_workspace_bytes(const cvd_model* const* models, int32_t np, const cvd_code* enc1,
                                                const int64_t* N, int32_t nN, int64_t batch, int32_t path) {
   if (!models || np <= 0 || !enc1 || !N || nN <= 0 || batch <= 0) return -1;
-  bool need = false;
+  int32_t need = 0;   // grid points that run generator + detector (one stream slot each)
   for (int32_t i = 0; i < np; ++i) {
     if (!models[i]) return -1;
-    need = need || !mc_run_fused(*models[i], path);
+    need += mc_run_fused(*models[i], path) ? 0 : 1;
   }
-  if (!need) return 0;   // every point runs the fused kernel
   int64_t best = 0;
   for (int32_t j = 0; j < nN; ++j) {
     if (N[j] < 0) return -1;
     best = std::max(best, cvd_mc_workspace_bytes(enc1, N[j], batch));
   }
-  return best;
+  return best * need;
 }
 
 extern "C" int cvd_mc_run_grid(const cvd_model* const* models, const cvd_code* enc1, const cvd_code* enc2,
                                const double* p, int32_t np, const int64_t* N, int32_t nN, uint64_t seed,
                                int64_t trial_begin, int64_t trial_end, int64_t batch, void* d_work,
                                int64_t* d_counts, int32_t path, void* stream) {
-  if (!models || !p || !N || np <= 0 || nN <= 0 || !d_counts) {
+  if (!models || !p || !N || np <= 0 || nN <= 0 || !d_counts || trial_end < trial_begin || batch <= 0) {
     set_error("bad mc_run_grid arguments");
     return CVD_E_INVALID;
   }
-  for (int32_t i = 0; i < np; ++i)
+  CodeDesc e1, e2;
+  int rc;
+  if ((rc = parse_code_dev(enc1, e1)) || (rc = parse_code_dev(enc2, e2))) return rc;
+  std::vector<int32_t> two;   // grid points on generator + detector (the others run the fused kernel)
+  for (int32_t i = 0; i < np; ++i) {
     if (!models[i]) { set_error("mc_run_grid: null model"); return CVD_E_INVALID; }
+    if (!(p[i] >= 0.0 && p[i] <= 1.0)) { set_error("p must lie in [0, 1]"); return CVD_E_INVALID; }
+    if (e1.n != models[i]->dec.n || e2.n != models[i]->dec.n || e1.k != models[i]->dec.k || e2.k != models[i]->dec.k) {
+      set_error("encoder and decoder must share (k, n)");
+      return CVD_E_INVALID;
+    }
+    if ((rc = check_device(*models[i]))) return rc;
+    if (!mc_run_fused(*models[i], path)) two.push_back(i);
+  }
+  int64_t nmax = 0;
+  for (int32_t j = 0; j < nN; ++j) {
+    if (N[j] < 0) { set_error("N must be >= 0"); return CVD_E_INVALID; }
+    nmax = std::max(nmax, N[j]);
+  }
+  if (!two.empty() && !d_work) {
+    set_error("cvd_mc_run_grid: these models and path need the stream workspace (cvd_mc_grid_workspace_bytes)");
+    return CVD_E_INVALID;
+  }
+  const int64_t slot = cvd_mc_workspace_bytes(enc1, nmax, batch);   // bytes per grid point's batch
+  const int32_t k = (int32_t)two.size();
+  std::vector<const cvd_model*> ms(k);
+  std::vector<const uint32_t*> rs(k);
+  std::vector<int64_t> ns(k), nh(k);
+  std::vector<int64_t*> cs(k);
   // Pd_plotter.py:196-233: N outer, p inner, num_iter trials at every point; the point
-  // (N[j], p[i]) accumulates into d_counts[(j * np + i) * 2 .. + 1]
-  for (int32_t j = 0; j < nN; ++j)
-    for (int32_t i = 0; i < np; ++i) {
-      const int rc = cvd_mc_run(models[i], enc1, enc2, p[i], N[j], seed, trial_begin, trial_end, batch, d_work,
-                                d_counts + 2 * ((int64_t)j * np + i), path, stream);
+  // (N[j], p[i]) accumulates into d_counts[(j * np + i) * 2 .. + 1].  The p row of one N
+  // runs batch by batch: every point's streams generated into its own workspace slot,
+  // then ONE cvd_detect_multi over the row (the models sharing the specialised kernel
+  // variant in one launch, so a row of small batches pays one last-round tail)
+  for (int32_t j = 0; j < nN; ++j) {
+    for (int32_t i = 0; i < np; ++i)
+      if (mc_run_fused(*models[i], path)) {
+        rc = cvd_mc_run(models[i], enc1, enc2, p[i], N[j], seed, trial_begin, trial_end, batch, nullptr,
+                        d_counts + 2 * ((int64_t)j * np + i), path, stream);
+        if (rc) return rc;
+      }
+    if (k == 0) continue;
+    for (int64_t b = trial_begin; b < trial_end; b += batch) {
+      const int64_t T = std::min(batch, trial_end - b);
+      for (int32_t x = 0; x < k; ++x) {
+        const int32_t i = two[x];
+        uint32_t* r = reinterpret_cast<uint32_t*>(static_cast<char*>(d_work) + (size_t)x * (size_t)slot);
+        const uint32_t tag = grid_tag(N[j], p[i]);
+        const uint64_t thr = noise_threshold(p[i]);
+        if ((rc = launch_generate(e1, (uint32_t)seed, (uint32_t)(seed >> 32), tag, thr, N[j], 1, 2 * b, 2, r, 2 * T, 0,
+                                  T, stream)))
+          return rc;
+        if ((rc = launch_generate(e2, (uint32_t)seed, (uint32_t)(seed >> 32), tag, thr, N[j], 1, 2 * b + 1, 2, r,
+                                  2 * T, T, T, stream)))
+          return rc;
+        ms[x] = models[i]; rs[x] = r; ns[x] = 2 * T; nh[x] = T;
+        cs[x] = d_counts + 2 * ((int64_t)j * np + i);
+      }
+      rc = cvd_detect_multi(ms.data(), k, rs.data(), N[j], ns.data(), nh.data(), nullptr, cs.data(),
+                            path, stream);
       if (rc) return rc;
     }
+  }
   return CVD_OK;
 }

@@ -439,7 +439,10 @@ class Detector:
         T = int(trial_end) - int(trial_begin)
         if T <= 0:
             return counts
-        batch = self.default_batch(max(N_list), T) if batch is None else int(batch)
+        if batch is None:
+            # the p row's batches share the HBM budget (one stream slot per point)
+            free, _ = torch.cuda.mem_get_info(self.device)
+            batch = self.default_batch(max(N_list), T, min(free // 3, 96 << 30) // max(1, npn))
         hs = (ctypes.c_void_p * npn)(*[m.handle.value for m in models])
         pv = (ctypes.c_double * npn)(*[float(p) for p in p_list])
         Nv = (ctypes.c_int64 * nN)(*[int(N) for N in N_list])
@@ -483,19 +486,22 @@ def run_experiment(k, n, m, gen1, gen2, num_iter, p_vec, learn_len, learn_burn, 
     returns the same DataFrame.
     """
     import pandas as pd
-    from .distributed import run_sharded, pd_rows
+    from .distributed import run_sharded_grid, pd_rows
 
     det = _detector(k, n, m, gen1, device)
     N_spectrum = list(N_SPECTRUM_BY_M.get(m, [50, 100, 200]) if N_list is None else N_list)
 
-    det.prepare_models(list(p_vec), learn_len, learn_burn, laplace, seed)
+    models = det.prepare_models(list(p_vec), learn_len, learn_burn, laplace, seed)
 
-    def count_fn(iN, N, ip, p, lo, hi, out):
-        model = det.model(p, learn_len, learn_burn, laplace, seed)
-        det.run_trials(model, gen1, gen2, N, p, seed, lo, hi, batch=batch, path=path, counts=out,
-                       early_decision=early_decision)
+    def grid_fn(lo, hi, out):
+        # the whole (N, p) grid of this rank's trial block in one library call
+        # (cvd_mc_run_grid: per N, the p row's batches in multi-model launches)
+        det.run_grid(models, gen1, gen2, list(p_vec), N_spectrum, seed, lo, hi, batch=batch, path=path,
+                     counts=out, early_decision=early_decision)
 
-    counts = run_sharded(count_fn, N_spectrum, list(p_vec), num_iter, det.device)
+    counts = run_sharded_grid(grid_fn, N_spectrum, list(p_vec), num_iter, det.device)
+    for mdl in models:
+        mdl.device_error()
     return pd.DataFrame(pd_rows(counts, N_spectrum, list(p_vec), num_iter))
 
 

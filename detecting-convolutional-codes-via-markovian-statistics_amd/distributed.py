@@ -44,6 +44,22 @@ def run_sharded(count_fn, N_list, p_vec, num_iter, device, rank=None, world=None
     return counts
 
 
+def run_sharded_grid(grid_fn, N_list, p_vec, num_iter, device, rank=None, world=None):
+    """The same with the whole grid in one call: grid_fn(lo, hi, counts) accumulates this
+    rank's trial block [lo, hi) of EVERY (N, p) point into counts[nN, np, 2] (e.g.
+    Detector.run_grid, cvd_mc_run_grid), then one all_reduce."""
+    import torch.distributed as tdist
+    r0, w0 = dist_info()
+    rank = r0 if rank is None else rank
+    world = w0 if world is None else world
+    counts = torch.zeros((len(N_list), len(p_vec), 2), dtype=torch.int64, device=device)
+    lo, hi = shard(num_iter, rank, world)
+    grid_fn(lo, hi, counts)
+    if tdist.is_available() and tdist.is_initialized():
+        tdist.all_reduce(counts, op=tdist.ReduceOp.SUM)
+    return counts
+
+
 def allreduce_counts(tensors, streams=None):
     """SUM-reduce int64 count tensors, one per device of this process, in place
     through the C-ABI's RCCL entry (cvd_allreduce_counts: ncclCommInitAll + one

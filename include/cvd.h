@@ -244,9 +244,14 @@ int cvd_mc_run(const cvd_model* model, const cvd_code* enc1, const cvd_code* enc
  * num_iter per point; a shard of them under trial sharding), with models[i] the model
  * learned at p[i] (learn_P1_empirical is per p, Pd_plotter.py:123-169).  Point
  * (N[j], p[i]) accumulates into d_counts[(j*np + i)*2 + {0: H1, 1: H2}] -- the
- * [nN][np][2] count tensor cvd_allreduce_counts reduces -- exactly as np * nN
- * cvd_mc_run calls would.  d_work: cvd_mc_grid_workspace_bytes (the largest N's
- * workspace; 0 = NULL allowed when every point runs the fused kernel). */
+ * [nN][np][2] count tensor cvd_allreduce_counts reduces -- exactly the counts np * nN
+ * cvd_mc_run calls give.  The p row of one N runs batch by batch: every point's streams
+ * are generated into its own workspace slot, then one cvd_detect_multi detects the row
+ * (the models sharing the specialised kernel variant in one launch, so a row of small
+ * batches -- the reference's num_iter = 10,000 per point -- pays one last-round tail,
+ * not one per p); points whose model runs the fused kernel (CVD_PATH_AUTO, mc_fused)
+ * run it without a slot.  d_work: cvd_mc_grid_workspace_bytes (one slot of the largest
+ * N's batch per non-fused point; 0 = NULL allowed when every point runs fused). */
 int64_t cvd_mc_grid_workspace_bytes(const cvd_model* const* models, int32_t np, const cvd_code* enc1,
                                     const int64_t* N, int32_t nN, int64_t batch, int32_t path);
 int cvd_mc_run_grid(const cvd_model* const* models, const cvd_code* enc1, const cvd_code* enc2,

@@ -54,8 +54,9 @@ def main(src, name):
                 d["_kernel"] = r["Kernel_Name"]
     cfg = bench["config"]
     p_grid = cfg.get("p_grid", [None])
-    B, N = cfg["trials_per_step_per_gpu"], cfg["N"]
-    alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+    # trials per launch of one grid point (round 4: a step runs every p of the grid)
+    B, N = cfg.get("trials_per_p_per_step_per_gpu", cfg["trials_per_step_per_gpu"]), cfg["N"]
+    alg = B * 2 * ((N * cfg.get("n", 2) + 7) // 8)   # the packed streams, per grid point
     by_p = {}
     for tag, disp in det_rows.items():
         for i, did in enumerate(sorted(disp)):
@@ -66,6 +67,9 @@ def main(src, name):
                 e["counters"][k] = e["counters"].get(k, 0.0) + v
                 e["launches"][k] = e["launches"].get(k, 0) + 1
     ms_by_p = bench["diagnostic"].get("detector_ms_by_p", {})
+    for e in bench["diagnostic"].get("detector_ms_by_launch", []):   # round 4: per launch group
+        if len(e["p"]) == 1:
+            ms_by_p[str(e["p"][0])] = e["ms"]
 
     def derive(c, ms=None):
         # per wave-step figures over the launch's own waves (2 B sequences, 64 per wave):
@@ -109,7 +113,7 @@ def main(src, name):
     gen_per = {k: sum(v) / len(v) for k, v in gen.items()}
     out = {
         "kernel": bench["roofline"]["kernel"],
-        "workload": f"bench.py --config {cfg.get('name')} --steps {len(p_grid)} --warmup 0: one launch per p of "
+        "workload": f"bench.py --config {cfg.get('name')} --steps 1 --warmup 0 --multi 0: one launch per p of "
                     f"{p_grid}, {B} trials x 2 sequences, N = {N}",
         "source": "rocprofv3 --pmc, one counter group per pass (profiles/collect_sweep.sh), per detector launch",
         "per_p": per_p,

@@ -30,7 +30,7 @@ def _worker(rank, world, port, out_path):
     from __graft_entry__ import load_package
     from oracle import c_oracle as C
     pkg = load_package()
-    from dccvm_amd.distributed import run_sharded, pd_rows  # noqa: F401
+    from dccvm_amd.distributed import run_sharded, run_sharded_grid, pd_rows  # noqa: F401
     cc = pkg.CONFIG_CODES["m2"]
     c1, c2 = C.Code(cc["gen1"], 2, 1, 2), C.Code(cc["gen2"], 2, 1, 2)
     models = {}
@@ -42,8 +42,15 @@ def _worker(rank, world, port, out_path):
         out += torch.from_numpy(cnt)
 
     counts = run_sharded(count_fn, [60, 120], [0.02, 0.1], 101, torch.device("cpu"))
+
+    def grid_fn(lo, hi, out):     # the grid form run_experiment uses (one call per rank)
+        for iN, N in enumerate([60, 120]):
+            for ip, p in enumerate([0.02, 0.1]):
+                count_fn(iN, N, ip, p, lo, hi, out[iN, ip])
+
+    grid = run_sharded_grid(grid_fn, [60, 120], [0.02, 0.1], 101, torch.device("cpu"))
     if rank == 0:
-        np.save(out_path, counts.numpy())
+        np.save(out_path, np.stack([counts.numpy(), grid.numpy()]))
     dist.destroy_process_group()
 
 
@@ -62,7 +69,9 @@ def test_sharded_counts_equal_single_process(pkg, tmp_path, world):
     out = str(tmp_path / "counts.npy")
     mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True,
                        start_method="spawn")
-    got = np.load(out)
+    both = np.load(out)
+    assert np.array_equal(both[0], both[1])          # run_sharded == run_sharded_grid
+    got = both[0]
     cc = pkg.CONFIG_CODES["m2"]
     c1, c2 = C.Code(cc["gen1"], 2, 1, 2), C.Code(cc["gen2"], 2, 1, 2)
     for iN, N in enumerate([60, 120]):

@@ -24,23 +24,26 @@ def _points(det, models, cc, p_list, N_list, lo, hi, **kw):
     return out
 
 
-@pytest.mark.parametrize("config", ["m2", "m6"])
-def test_grid_equals_per_point_calls(pkg, config):
+@pytest.mark.parametrize("config,path", [("m2", 0), ("m2", 1), ("m6", 0), ("r23_m4", 0)])
+def test_grid_equals_per_point_calls(pkg, config, path):
+    """path 0 = PATH_AUTO (m2: the fused kernel; m6: generator + one multi-model detect per
+    batch of the p row), 1 = PATH_TABLE (two kernels, one detect per point)"""
     cc = pkg.CONFIG_CODES[config]
     det = pkg.Detector(cc["k"], cc["n"], cc["m"], cc["gen1"], device=0)
     p_list, N_list = [0.02, 0.1, 0.2], [300, 1237]
     ll = 200_000 if config == "m6" else None
     models = [det.model(p, ll, 200, 1.0, SEED) for p in p_list]
     lo, hi = 1_000_003, 1_000_003 + 700          # not whole waves, offset ids
-    ref = _points(det, models, cc, p_list, N_list, lo, hi, batch=256)
-    got = det.run_grid(models, cc["gen1"], cc["gen2"], p_list, N_list, SEED, lo, hi, batch=256)
+    ref = _points(det, models, cc, p_list, N_list, lo, hi, batch=256, path=path)
+    got = det.run_grid(models, cc["gen1"], cc["gen2"], p_list, N_list, SEED, lo, hi, batch=256, path=path)
     assert np.array_equal(got.cpu().numpy(), ref)
     # early decision: the same counts
     early = det.run_grid(models, cc["gen1"], cc["gen2"], p_list, N_list, SEED, lo, hi, batch=256,
-                         early_decision=True)
+                         early_decision=True, path=path)
     assert np.array_equal(early.cpu().numpy(), ref)
     # accumulates into the caller's tensor like cvd_mc_run
-    got2 = det.run_grid(models, cc["gen1"], cc["gen2"], p_list, N_list, SEED, lo, hi, batch=256, counts=got)
+    got2 = det.run_grid(models, cc["gen1"], cc["gen2"], p_list, N_list, SEED, lo, hi, batch=256, counts=got,
+                        path=path)
     assert np.array_equal(got2.cpu().numpy(), 2 * ref)
     for mdl in models:
         assert mdl.device_error() == 0
@@ -58,7 +61,7 @@ def test_grid_workspace_and_null_workspace(pkg):
     hs = (ctypes.c_void_p * 2)(*[m.handle.value for m in mods])
     Nv = (ctypes.c_int64 * 2)(100, 10_000)
     assert lib.cvd_mc_grid_workspace_bytes(hs, 2, g1.c, Nv, 2, 4096, pkg.PATH_AUTO) == 0
-    assert lib.cvd_mc_grid_workspace_bytes(hs, 2, g1.c, Nv, 2, 4096, pkg.PATH_TABLE) == \
+    assert lib.cvd_mc_grid_workspace_bytes(hs, 2, g1.c, Nv, 2, 4096, pkg.PATH_TABLE) == 2 * \
         lib.cvd_mc_workspace_bytes(g1.c, 10_000, 4096)
     m6 = pkg.CONFIG_CODES["m6"]
     d6 = pkg.Detector(1, 2, 6, m6["gen1"], device=0)
