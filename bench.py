@@ -46,7 +46,6 @@ sys.path.insert(0, ROOT)
 METRIC = "MC trials/sec at N=1e5, rate-1/2 m=6 pair, 1/2/4/8 GPUs; Pd match vs CPU"
 P_GRID = [0.01, 0.02, 0.05, 0.10, 0.15, 0.20]
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-LDS_PEAK_GBS = 256 * 256 * 2.4   # 256 CUs x 256 B/clk (ds_read_b64, MI355X_MICROARCH.md LDS) x 2.4 GHz
 # VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
 SHADER_GHZ = 2.4
@@ -462,13 +461,21 @@ def main():
     alg_bytes = B * 2 * ((N * n + 7) // 8)               # one grid point's batch
     alg_launch = len(groups[gdom]) * alg_bytes
     achieved = alg_launch / (det_ms * 1e-3) / 1e9
-    if a.fused:
-        # no stream in HBM: the fused kernel is bound by its LDS gathers (per sequence-step
-        # one 16-bit record and two f64 entries, 18 B) and the generator's VALU; LDS peak
-        # 256 B/clk/CU (MI355X_MICROARCH.md, LDS: ds_read_b64) x 256 CUs x 2.4 GHz
-        alg_bytes = B * 2 * N * 18
-        alg_launch = len(groups[gdom]) * alg_bytes
-        achieved = alg_launch / (det_ms * 1e-3) / 1e9
+    # Dense-table kernels (C1 fused, C3 table16): bound by the LDS array, measured --
+    # SQ_LDS_IDX_ACTIVE over the launch's CU-cycles, and the share of it that is bank-
+    # conflict cycles (profiles/lds_bound.py over the r04_lds_pmc.sh passes).  The roofline
+    # keeps SURVEY §8(d)'s stream bytes (which the fused kernel never writes to HBM: it is
+    # the figure the §8(d) fraction is defined on) and carries the LDS counters beside it.
+    lds_diag = None
+    lds_path = os.path.join(ROOT, "profiles", f"pmc_lds_{a.config}.json")
+    if not parity and info["kind"] == 0 and os.path.exists(lds_path):
+        with open(lds_path) as f:
+            ld = json.load(f)
+        lds_diag = {k: ld[k] for k in ("kernel", "lds_busy", "lds_conflict_frac", "lds_array_cycles_per_lds_inst",
+                                        "valu_issue_2cyc", "source")}
+        lds_diag["meaning"] = ("lds_busy = SQ_LDS_IDX_ACTIVE / (256 CUs x kernel cycles); lds_conflict_frac = "
+                               "SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; valu_issue_2cyc = SQ_INSTS_VALU x 2 / "
+                               "(1024 SIMDs x kernel cycles)")
     traffic, traffic_src, pmc = None, None, None
     if a.pmc_traffic is None:
         a.pmc_traffic = os.path.join(ROOT, "profiles", f"pmc_{a.detector}_{a.config}.json")
@@ -555,13 +562,14 @@ def main():
                    "model": info["kind"] and "sparse(learned)" or "dense",
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
-        "roofline": {"bound": "lds" if a.fused else "valu" if valu else "hbm", "achieved": achieved,
-                     "peak": LDS_PEAK_GBS if a.fused else HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / (LDS_PEAK_GBS if a.fused else HBM_PEAK_GBS),
+        "roofline": {"bound": "lds" if lds_diag else "valu" if valu else "hbm", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "lds": lds_diag,
                      "traffic": traffic,
                      "kernel": ("parity_kernel (parity-template baseline, cvd_parity.hip)" if parity
                                 else "mc_table16_kernel (generator + LDS table automaton fused, cvd_mc_fused; "
-                                     "achieved = LDS gather bytes)" if a.fused
+                                     "achieved = SURVEY 8(d) stream bytes, which stay on chip)" if a.fused
                                 else pkg.KERNEL_NAMES[info["explicit_kernel"]] if info["kind"]
                                 else "detect_table_kernel (enumerated state automaton)"),
                      "traffic_source": traffic_src,

@@ -113,7 +113,7 @@ def main(src, name):
     gen_per = {k: sum(v) / len(v) for k, v in gen.items()}
     out = {
         "kernel": bench["roofline"]["kernel"],
-        "workload": f"bench.py --config {cfg.get('name')} --steps 1 --warmup 0 --multi 0: one launch per p of "
+        "workload": f"bench.py --config {cfg.get('name')} --steps {len(p_grid)} --warmup 0: one launch per p of "
                     f"{p_grid}, {B} trials x 2 sequences, N = {N}",
         "source": "rocprofv3 --pmc, one counter group per pass (profiles/collect_sweep.sh), per detector launch",
         "per_p": per_p,
