@@ -492,9 +492,11 @@ def main():
         # launch-weighted mean over the sweep, per trial of the PMC run's launches (whole
         # residency rounds like this run's) times this run's trials per launch
         pmc_scale = B / float(pmc.get("batch") or B)
-        # the dominant launch's traffic: the FETCH of its grid points' single-p launches
+        # per launch: --sweep per-p, the launch-weighted mean over the sweep (each p one launch,
+        # like `value`'s weighting); --sweep all, the FETCH of the dominant launch's grid points
         try:
-            traffic = sum(pmc["per_p"][str(p_grid[i])]["fetch_bytes"] for i in groups[gdom]) * pmc_scale
+            traffic = (sum(pmc["per_p"][str(p_grid[i])]["fetch_bytes"] for i in groups[gdom]) if sweep_all
+                       else pmc["detector_fetch_bytes_per_launch"]) * pmc_scale
         except (KeyError, TypeError):
             traffic = None
         traffic_by_p = {p: {"fetch_bytes": e["fetch_bytes"] * pmc_scale, "fetch_x_algorithmic": e["fetch_x_algorithmic"],
