@@ -133,6 +133,23 @@ def parse():
     return ap.parse_args()
 
 
+def sweep_value(step_ms, npg, B, world, sweep_all=False):
+    """Trials/s of a p sweep from the timed steps' durations (ms, max over ranks).
+    Per-p steps (step s at p_grid[s % npg], B trials per rank): B x ranks / (the mean over
+    the p of the mean step time at p), so every p weighs the same however many steps each
+    p got (Pd_plotter.py:199-233 runs num_iter trials at every p).  Sweep steps (every p
+    in every step): trials / total time.  Returns (value, indices of the p covered)."""
+    import numpy as np
+    if not step_ms:
+        raise ValueError("no timed steps")
+    if sweep_all:
+        return world * npg * B / (float(np.mean(step_ms)) * 1e-3), list(range(npg))
+    by = {}
+    for s, t in enumerate(step_ms):
+        by.setdefault(s % npg, []).append(t)
+    return world * B / (float(np.mean([np.mean(v) for v in by.values()])) * 1e-3), sorted(by)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -350,13 +367,7 @@ def main():
         return out
 
     def weighted_value(st_ms, steps):
-        """per-p mode: B x ranks / mean over the p of the mean step time at p; all: trials / time"""
-        if sweep_all:
-            return world * npg * B / (np.mean(st_ms) * 1e-3), list(range(npg))
-        by = {}
-        for s in range(steps):
-            by.setdefault(s % npg, []).append(st_ms[s])
-        return world * B / (np.mean([np.mean(v) for v in by.values()]) * 1e-3), sorted(by)
+        return sweep_value(st_ms[:steps], npg, B, world, sweep_all)
 
     # warmup steps use trial ids far from the timed ones (base 10,000 steps)
     run(a.warmup, 10_000)
