@@ -247,11 +247,6 @@ __device__ __forceinline__ void fill_filter_patterns() {
 // into VGPRs, two v_mov per step): 211 -> 209 static VALU per step, still 126 VGPRs;
 // p = 0.05 / 0.1 / 0.2 675.5 / 705.6 / 678.7 -> 674.1 / 703.8 / 676.3 ms per 655,360-trial
 // launch, walk-mode p within 1 ms (profiles/r03v/ab_lpu.txt)
-// timing-study toggle (round 4 A/B, results identical): the zero-nibble test accumulated
-// by one v_bitop3 per key word (static VALU per step 208.75 -> 206.75)
-#ifndef CVD_K1B_ZN_CHAIN
-#define CVD_K1B_ZN_CHAIN 0
-#endif
 #ifndef CVD_K1B_LPU_VGPR
 #define CVD_K1B_LPU_VGPR 1
 #endif
@@ -639,16 +634,7 @@ __device__ __forceinline__ void k1b_acs(const ExpArgs& a, cu32* tb, RowCursor<(1
     // the step minimum 0; specialised: the pairs already are D + 1 + mu (1..15) and
     // a nibble < 2 (hasless(v, 2): existence is exact) is the step minimum 0
     const uint32_t v = kSpec ? x + (y << 4) : x + (y << 4) - O8;
-#if CVD_K1B_ZN_CHAIN
-    // zn = ((v - K) & ~v) | zn as one v_bitop3 (truth table 0xBA over (t, v, zn)): the
-    // accumulation rides in the test instead of or3 reductions
-    {
-      const uint32_t t = v - (kSpec ? 0x22222222u : 0x11111111u);
-      asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xba" : "+v"(zn) : "v"(t), "v"(v));
-    }
-#else
     zn |= (v - (kSpec ? 0x22222222u : 0x11111111u)) & ~v;
-#endif
     kw[w] = v;
   };
   if constexpr (kKind == 1) {
