@@ -172,6 +172,17 @@ __device__ __forceinline__ uint32_t spread_n(uint32_t x) {   // bit i -> bit n*i
   }
 }
 
+// Rate 2/3 (k = 2, n = 3): the flat input bits of a word (bit 2t + r = u_r(t), t < 10)
+// moved to the received word's stride (bit 3t + r): pairs t move up by t, one stage per
+// bit of t (8, 4, 2, 1), three VALU each.  Lane 2 of every step stays 0.
+__device__ __forceinline__ uint32_t spread23(uint32_t x) {
+  x &= 0xFFFFFu;
+  x = (x & 0x0000FFFFu) | ((x << 8) & 0x0F000000u);   // t = 8, 9: bits 16..19 -> 24..27
+  x = (x & 0x0F0000FFu) | ((x << 4) & 0x000FF000u);   // t = 4..7: 8..15 -> 12..19
+  x = (x & 0x0F00F00Fu) | ((x << 2) & 0x003C03C0u);   // t & 2: +2
+  return (x & 0x030C30C3u) | ((x << 1) & 0x18618618u);   // t & 1: +1 -> bit 3t + r
+}
+
 __device__ __forceinline__ uint32_t even_bits(uint32_t x) {   // bit 2i -> bit i
   x &= 0x55555555u;
   x = (x | (x >> 1)) & 0x33333333u;
@@ -347,6 +358,18 @@ struct ChunkEncoder {
   // rate-2/3 generator faster alone (16.1 -> 15.8 ms) but the overlapped C3 step
   // 1.7% slower (profiles/r02z_gen/ab_enc_*.json).
   static constexpr bool kSpreadFirst = k == 1;
+  // k = 2, n = 3 (C3): the flat input bits go to the word's stride in one spread
+  // (spread23: bit 2t + r -> 3t + r) and the window X = (this word << 30 | the previous
+  // word) is 60 bits, so every tap u_r(t - d) of output j is one v_alignbit by
+  // 30 - 3 d + r - j of X, landing on lane j of the word; the other phase's bits land on
+  // lanes j +- 1 and lane 2 of X is empty, so one AND per output keeps lane j.  No
+  // even/odd split of the inputs and no spread per output: 173 -> ~130 VALU per stream
+  // word (profiles/pmc_markov_r23_m4.json).  CVD_GEN_K2_STRIDE3=0 restores the per-phase
+  // windows (same streams).
+#ifndef CVD_GEN_K2_STRIDE3
+#define CVD_GEN_K2_STRIDE3 1
+#endif
+  static constexpr bool kStride3 = CVD_GEN_K2_STRIDE3 && k == 2 && n == 3;
   const GenArgs* a;
   uint32_t slo, ihi;
   int64_t iblk;
@@ -368,8 +391,8 @@ struct ChunkEncoder {
     }
     return u4_get(iv, (uint32_t)(W & 3));
   }
-  // input bits [w*SPW*k, (w+1)*SPW*k) of the flat input stream, split by phase
-  __device__ void word_inputs(int64_t w, uint32_t (&U)[k]) {
+  // input bits [w*SPW*k, (w+1)*SPW*k) of the flat input stream (bit SPW*k.. unmasked)
+  __device__ uint32_t flat_inputs(int64_t w) {
     uint32_t Fw = 0u;
     if (a->random_input) {
       const int64_t b0 = w * SPW * k;
@@ -378,6 +401,11 @@ struct ChunkEncoder {
       const uint32_t hi = (off + SPW * k > 32u) ? input_word((b0 >> 5) + 1) : 0u;
       Fw = off ? __builtin_amdgcn_alignbit(hi, lo, off) : lo;
     }
+    return Fw;
+  }
+  // the same split by phase
+  __device__ void word_inputs(int64_t w, uint32_t (&U)[k]) {
+    const uint32_t Fw = flat_inputs(w);
     if constexpr (k == 1) U[0] = Fw;
     else { U[0] = even_bits(Fw); U[1] = even_bits(Fw >> 1); }
 #pragma unroll
@@ -386,6 +414,10 @@ struct ChunkEncoder {
   }
   // history of a segment starting at word w0 > 0: the hs input steps before it
   __device__ void seek(int64_t w0) {
+    if constexpr (kStride3) {
+      sprev[0] = spread23(flat_inputs(w0 - 1));
+      return;
+    }
     uint32_t Up[k];
     word_inputs(w0 - 1, Up);
 #pragma unroll
@@ -396,6 +428,34 @@ struct ChunkEncoder {
   }
   __device__ uint32_t encode(int64_t w, uint32_t nm) {
     const int hs = a->hs;
+    if constexpr (kStride3) {
+      const uint32_t sc = spread23(flat_inputs(w));
+      const uint32_t xlo = (sc << 30) | sprev[0], xhi = sc >> 2;   // X = sc * 2^30 + previous word
+      sprev[0] = sc;
+      uint32_t word = 0u;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        uint32_t o = 0u;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          // window tap sh of phase r is u_r(t - (hs - sh)): X bit 30 + 3 (t - hs + sh) + r,
+          // moved to bit 3t + j (the scalar loop over the set taps, as below)
+          uint32_t tm = a->taps[j][r];
+          asm volatile("" : "+s"(tm));
+#pragma nounroll
+          while (tm) {
+            const uint32_t sh = (uint32_t)__builtin_ctz(tm);
+            tm &= tm - 1u;
+            o ^= __builtin_amdgcn_alignbit(xhi, xlo, 30u - 3u * (uint32_t)hs + 3u * sh + (uint32_t)r - (uint32_t)j);
+          }
+        }
+        word |= o & (0x09249249u << j);   // lane j of the 10 steps
+      }
+      word ^= nm;
+      const int64_t ns = a->N - w * SPW;         // steps in this word (last word: < SPW)
+      if (ns < SPW) word &= (1u << (n * ns)) - 1u;
+      return word;
+    }
     const uint32_t nhs = (uint32_t)(n * hs), nrest = (uint32_t)(n * (SPW - hs));   // 0 < nhs < 32, nrest < 32
     uint32_t U[k];
     word_inputs(w, U);
