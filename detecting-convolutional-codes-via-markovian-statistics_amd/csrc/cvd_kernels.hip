@@ -43,6 +43,12 @@ namespace {
 
 // ───────────────────────────── generator ────────────────────────────────────
 
+// k = 2, n = 3 encoder form of ChunkEncoder (1: stride-3 window, 0: per-phase windows)
+#ifndef CVD_GEN_K2_STRIDE3
+#define CVD_GEN_K2_STRIDE3 1
+#endif
+constexpr int kTapSlots = 10;     // longest unrolled tap list per output (m <= 8, k = 1: 9 taps)
+
 struct GenArgs {
   CodeDesc enc;
   uint32_t k0, k1, tag, thr_lo;
@@ -50,6 +56,13 @@ struct GenArgs {
   int32_t hs;                     // gen_fast_kernel: history steps ceil(m / k)
   uint32_t slots;                 // gen_fast_kernel: noise exchange slots per round (64; tests: fewer)
   uint32_t taps[kMaxN][2];        // gen_fast_kernel: shift set of output j on input phase r
+  // the same taps as window shifts (v_alignbit amounts), per output j, every unused slot
+  // a shift that moves only empty lanes of the window onto lane j (ChunkEncoder kT > 0):
+  // slot i in bits 5 (i % 6) of word i / 6 (v_alignbit reads the low 5 bits of its shift
+  // operand, so one s_lshr extracts a slot); ntap = the longest list (0: the form has no
+  // shift list, k = 2 per-phase windows)
+  uint32_t tpk[kMaxN][2];
+  int32_t ntap;
   int64_t N, seq_base, seq_stride, pitch, q0, count;
   uint32_t* r;
 };
@@ -344,7 +357,7 @@ __device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, uint32_t* su,
 // Encoder of one sequence, one received word at a time (bit-parallel, see above):
 // the input stream's Philox block cache and the window history carried from word
 // to word.  encode(w, nm) returns word w with the flip mask nm applied.
-template <int k, int n>
+template <int k, int n, int kT = 0>
 struct ChunkEncoder {
   static constexpr int SPW = 32 / n, NBITS = SPW * n;
   static constexpr uint32_t kValid = NBITS == 32 ? ~0u : (1u << (NBITS % 32)) - 1u;
@@ -366,10 +379,15 @@ struct ChunkEncoder {
   // even/odd split of the inputs and no spread per output: 173 -> ~130 VALU per stream
   // word (profiles/pmc_markov_r23_m4.json).  CVD_GEN_K2_STRIDE3=0 restores the per-phase
   // windows (same streams).
-#ifndef CVD_GEN_K2_STRIDE3
-#define CVD_GEN_K2_STRIDE3 1
-#endif
   static constexpr bool kStride3 = CVD_GEN_K2_STRIDE3 && k == 2 && n == 3;
+  // kT > 0 (spread-first and stride-3 forms): the taps of output j as a fixed list of kT
+  // window shifts (GenArgs::tsh, SGPRs), fully unrolled -- one v_alignbit per slot, the
+  // XORs as v_xor3, and no scalar loop (the loop over the set bits of the tap mask issues
+  // 7 SALU per tap: s_ff1, the mask update, the shift arithmetic, compare and branch).
+  // Padding slots move only empty lanes of the window onto lane j and the lane mask
+  // after the XOR removes what they move elsewhere.
+  static_assert(kT == 0 || kSpreadFirst || kStride3, "ChunkEncoder: tap lists need the spread window");
+  static_assert(kT <= kTapSlots, "ChunkEncoder: tap list");
   const GenArgs* a;
   uint32_t slo, ihi;
   int64_t iblk;
@@ -426,6 +444,22 @@ struct ChunkEncoder {
       else hist[r] = (Up[r] >> (SPW - a->hs)) & ((1u << a->hs) - 1u);
     }
   }
+  // output j's packed tap list (kT > 0), re-read per word: the asm keeps the compiler from
+  // hoisting the n kT extracted shifts out of the chunk loop into SGPRs (18 for rate 2/3:
+  // SGPR spills to VGPR lanes); per word the words and one s_lshr per slot
+  __device__ __forceinline__ void tap_words(int j, uint32_t& p0, uint32_t& p1) const {
+    p0 = a->tpk[j][0];
+    asm volatile("" : "+s"(p0));
+    p1 = 0u;
+    if constexpr (kT > 6) {
+      p1 = a->tpk[j][1];
+      asm volatile("" : "+s"(p1));
+    }
+  }
+  static __device__ __forceinline__ uint32_t tap_slot(int i, uint32_t p0, uint32_t p1) {
+    const uint32_t p = i < 6 ? p0 : p1;
+    return (i % 6) ? p >> (5 * (i % 6)) : p;   // v_alignbit uses the low 5 bits
+  }
   __device__ uint32_t encode(int64_t w, uint32_t nm) {
     const int hs = a->hs;
     if constexpr (kStride3) {
@@ -436,6 +470,14 @@ struct ChunkEncoder {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         uint32_t o = 0u;
+        if constexpr (kT > 0) {
+          uint32_t p0, p1;
+          tap_words(j, p0, p1);
+#pragma unroll
+          for (int i = 0; i < kT; ++i) o ^= __builtin_amdgcn_alignbit(xhi, xlo, tap_slot(i, p0, p1));
+          word |= o & (0x09249249u << j);
+          continue;
+        }
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
           // window tap sh of phase r is u_r(t - (hs - sh)): X bit 30 + 3 (t - hs + sh) + r,
@@ -477,6 +519,16 @@ struct ChunkEncoder {
 #pragma unroll
     for (int j = 0; j < n; ++j) {
       uint32_t o = 0u;
+      if constexpr (kT > 0) {   // spread-first (k = 1): lane 0 of the window, stride n
+        static_assert(n == 2 || n == 3, "ChunkEncoder: spread-first tap lists for n = 2, 3");
+        constexpr uint32_t kLane0 = n == 2 ? 0x55555555u : 0x09249249u;   // bits n i, i < SPW
+        uint32_t p0, p1;
+        tap_words(j, p0, p1);
+#pragma unroll
+        for (int i = 0; i < kT; ++i) o ^= __builtin_amdgcn_alignbit(hi[0], lo[0], tap_slot(i, p0, p1));
+        word |= (o & kLane0) << j;
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < k; ++r) {
         // the set taps only, as a scalar loop over the uniform mask (s_ff1):
@@ -543,7 +595,7 @@ struct ChunkEncoder {
   }
 };
 
-template <int k, int n>
+template <int k, int n, int kT>
 __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   constexpr int SPW = 32 / n;
   static_assert(k >= 1 && k <= 2 && SPW * k <= 32, "gen_fast_kernel: shape");
@@ -561,7 +613,7 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   auto seq = [&](uint32_t l) { return make_uint2(nl.slo[l], nl.nhi[l]); };
   const int64_t nwords = (a.N + SPW - 1) / SPW;
   const int64_t nw4 = (nwords + 3) & ~(int64_t)3;
-  ChunkEncoder<k, n> enc;
+  ChunkEncoder<k, n, kT> enc;
   enc.init(&a, sid);
   // segment blockIdx.y of the sequence's 16-byte chunks: every word depends only
   // on its own inputs and the hs input steps before it, so segments are
@@ -777,7 +829,7 @@ struct FusedArgs {
   int64_t trial_begin, T, Tp;
 };
 
-template <int k, int n, int BS, bool kLr>
+template <int k, int n, int BS, bool kLr, int kT = 0>
 __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
   constexpr int SPW = 32 / n;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -802,7 +854,7 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
     const uint64_t sd = sid0 + 2 * (uint64_t)l;
     return make_uint2((uint32_t)sd, ctr_hi(sd, kKindNoise));
   };
-  ChunkEncoder<k, n> enc;
+  ChunkEncoder<k, n, kT> enc;
   enc.init(&g, sid0 + 2 * (uint64_t)lane);
   const uint2 own = seq(lane);
   const int64_t N = ta.N, nwords = (N + SPW - 1) / SPW, nchunks = (nwords + 3) / 4;
@@ -848,7 +900,7 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
         }
 #pragma unroll
         for (int r = SPW; r < 10; ++r) { philox_round<2>(xv, k0, k1); k0 += kPhiloxW0; k1 += kPhiloxW1; }
-        noise_head_planes(g, xv, valid && wn + e < nwords, ChunkEncoder<k, n>::kValid, U[e], F[e]);
+        noise_head_planes(g, xv, valid && wn + e < nwords, ChunkEncoder<k, n, kT>::kValid, U[e], F[e]);
       }
     } else {
       for (int e = 0; e < 4; ++e) {
@@ -1287,6 +1339,30 @@ GenArgs gen_args(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, ui
       for (int b = 0; b < enc.m; ++b)                              // s bit b = u_{b%k}(t - 1 - b/k)
         if ((g >> (1 + b)) & 1u) a.taps[j][b % enc.k] ^= 1u << (a.hs - 1 - b / enc.k);
     }
+  // the taps as window shifts (ChunkEncoder::encode): spread-first (k = 1) window tap sh
+  // is n sh; stride-3 (k = 2, n = 3) tap sh of phase r is 30 - 3 hs + 3 sh + r - j.
+  // Padding: k = 1 shifts by 1 (lane 0 of the result reads an empty lane; the lane mask
+  // drops what lands elsewhere), stride 3 by 5 - j (lane j reads the empty lane 2).
+  a.ntap = 0;
+  const bool stride3 = CVD_GEN_K2_STRIDE3 && enc.k == 2 && enc.n == 3;
+  for (int j = 0; j < kMaxN; ++j) a.tpk[j][0] = a.tpk[j][1] = 0u;
+  if ((enc.k == 1 && (enc.n == 2 || enc.n == 3)) || stride3) {
+    for (int j = 0; j < enc.n; ++j) {
+      uint32_t sl[kTapSlots];
+      int c = 0;
+      for (int r = 0; r < enc.k; ++r)
+        for (int sh = 0; sh < 32; ++sh)
+          if ((a.taps[j][r] >> sh) & 1u) {
+            const uint32_t s = stride3 ? (uint32_t)(30 - 3 * a.hs + 3 * sh + r - j) : (uint32_t)(enc.n * sh);
+            if (c < kTapSlots) sl[c] = s;
+            ++c;
+          }
+      a.ntap = std::max(a.ntap, c);
+      for (; c < kTapSlots; ++c) sl[c] = stride3 ? (uint32_t)(5 - j) : 1u;
+      for (int i = 0; i < kTapSlots; ++i) a.tpk[j][i / 6] |= (sl[i] & 31u) << (5 * (i % 6));
+    }
+    if (a.ntap > kTapSlots) a.ntap = 0;
+  }
   {
     // test knob: fewer noise exchange slots per round, so the multi-round path runs
     const char* e = std::getenv("CVD_GEN_SLOTS");
@@ -1299,6 +1375,29 @@ GenArgs gen_args(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t tag, ui
 bool gen_fast_ok(const CodeDesc& enc) {
   return !std::getenv("CVD_GEN_GENERIC") && enc.m <= kMaxM && enc.k <= 2 &&
          (enc.m + enc.k - 1) / enc.k + 32 / std::max(enc.n, 1) <= 32;
+}
+
+// unrolled tap-list length for encoders with at most `ntap` taps per output: the
+// instantiated lengths (3..6, 8), 0 = the scalar loop over the tap masks (longer lists,
+// the k = 2 per-phase form, or CVD_GEN_TAP_LOOP=1)
+int tap_slots(int ntap) {
+  if (ntap <= 0 || std::getenv("CVD_GEN_TAP_LOOP")) return 0;
+  for (int t : {3, 4, 5, 6, 8})
+    if (ntap <= t) return t;
+  return 0;
+}
+
+template <int k, int n>
+void (*gen_fast_variant(int kt))(GenArgs) {
+  if constexpr (k == 2 && !CVD_GEN_K2_STRIDE3) return gen_fast_kernel<k, n, 0>;
+  switch (kt) {
+    case 3: return gen_fast_kernel<k, n, 3>;
+    case 4: return gen_fast_kernel<k, n, 4>;
+    case 5: return gen_fast_kernel<k, n, 5>;
+    case 6: return gen_fast_kernel<k, n, 6>;
+    case 8: return gen_fast_kernel<k, n, 8>;
+    default: return gen_fast_kernel<k, n, 0>;
+  }
 }
 }  // namespace
 
@@ -1320,9 +1419,10 @@ int cvd::launch_generate(const CodeDesc& enc, uint32_t k0, uint32_t k1, uint32_t
     const int64_t seg = std::max<int64_t>(1, std::min<int64_t>((16 * 1024 + waves - 1) / waves, nchunks / 16));
     gdim.y = (unsigned)std::min<int64_t>(seg, 65535);
   }
-  if (fast && enc.k == 1 && enc.n == 2) kern = gen_fast_kernel<1, 2>;
-  else if (fast && enc.k == 1 && enc.n == 3) kern = gen_fast_kernel<1, 3>;
-  else if (fast && enc.k == 2 && enc.n == 3) kern = gen_fast_kernel<2, 3>;
+  const int kt = tap_slots(a.ntap);
+  if (fast && enc.k == 1 && enc.n == 2) kern = gen_fast_variant<1, 2>(kt);
+  else if (fast && enc.k == 1 && enc.n == 3) kern = gen_fast_variant<1, 3>(kt);
+  else if (fast && enc.k == 2 && enc.n == 3) kern = gen_fast_variant<2, 3>(kt);
   else if (enc.k == 1 && enc.n == 2) kern = gen_kernel<1, 2>;
   else if (enc.k == 1 && enc.n == 3) kern = gen_kernel<1, 3>;
   else if (enc.k == 2 && enc.n == 3) kern = gen_kernel<2, 3>;
@@ -1420,7 +1520,15 @@ int cvd::launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc&
   a.g[1] = gen_args(e2, k0, k1, tag, thr, N, 1);
   a.trial_begin = trial_begin; a.T = T; a.Tp = (T + 63) & ~(int64_t)63;
   void (*kern)(FusedArgs) = nullptr;
-  if (k == 1 && n == 2)
+  // unrolled tap lists for rate 1/2 (C1) with at most 3 or 5 taps per output
+  const int kt = tap_slots(std::max(a.g[0].ntap, a.g[1].ntap));
+  if (k == 1 && n == 2 && kt == 3)
+    kern = big ? mc_table16_kernel<1, 2, 1024, false, 3> : lr ? mc_table16_kernel<1, 2, kBlock, true, 3>
+                                                            : mc_table16_kernel<1, 2, kBlock, false, 3>;
+  else if (k == 1 && n == 2 && (kt == 4 || kt == 5))
+    kern = big ? mc_table16_kernel<1, 2, 1024, false, 5> : lr ? mc_table16_kernel<1, 2, kBlock, true, 5>
+                                                            : mc_table16_kernel<1, 2, kBlock, false, 5>;
+  else if (k == 1 && n == 2)
     kern = big ? mc_table16_kernel<1, 2, 1024, false> : lr ? mc_table16_kernel<1, 2, kBlock, true>
                                                          : mc_table16_kernel<1, 2, kBlock, false>;
   else if (k == 1 && n == 3)
