@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libcvd.so")
+# CVD_LIB_PATH: another build of the same ABI (A/B builds, profiles/build_ab.sh)
+LIB_PATH = os.environ.get("CVD_LIB_PATH") or os.path.join(_HERE, "lib", "libcvd.so")
 ABI_VERSION = 8
 
 PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5

@@ -47,6 +47,14 @@ namespace {
 #ifndef CVD_GEN_K2_STRIDE3
 #define CVD_GEN_K2_STRIDE3 1
 #endif
+// noise straggler exchange: one block per slot lane, a pair's two blocks on two lanes
+// (1), or both blocks of a pair on one slot lane (0)
+#ifndef CVD_GEN_XCHG_SPLIT
+#define CVD_GEN_XCHG_SPLIT 1
+#endif
+#ifndef CVD_FUSED_XCHG_SPLIT   // the same in the fused trial kernel (ChunkEncoder::finish)
+#define CVD_FUSED_XCHG_SPLIT 0
+#endif
 constexpr int kTapSlots = 10;     // longest unrolled tap list per output (m <= 8, k = 1: 9 taps)
 
 struct GenArgs {
@@ -214,17 +222,24 @@ __device__ __forceinline__ uint32_t even_bits(uint32_t x) {   // bit 2i -> bit i
 // compiles to a branch tree whose cases copy operands around; per-plane uniform
 // branches were if-converted into selects; the direct MSB-first form with masks
 // costs three VALU per plane.  Measured in profiles/r02z_gen.)
+// kLaneNib: `nib` differs between lanes (t in a VGPR; the split exchange below).
+template <bool kLaneNib = false>
 __device__ __forceinline__ void noise_planes4(uint32_t nib, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
                                               uint32_t& U, uint32_t& F) {
   const uint32_t r[4] = {r0, r1, r2, r3};
-  const uint32_t b = __builtin_amdgcn_readfirstlane(nib);
+  const uint32_t b = kLaneNib ? nib : __builtin_amdgcn_readfirstlane(nib);
   uint32_t lt = 0u, eq = U;
 #pragma unroll
   for (int i = 3; i >= 0; --i) {
     const uint32_t ti = 0u - ((b >> (3 - i)) & 1u);
     // lt = MAJ(~r, t, lt) (truth table 0x8E), eq &= ~(r ^ t) (0x90)
-    asm("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x8e" : "+v"(lt) : "v"(r[i]), "s"(ti));
-    asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x90" : "+v"(eq) : "v"(r[i]), "s"(ti));
+    if constexpr (kLaneNib) {
+      asm("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x8e" : "+v"(lt) : "v"(r[i]), "v"(ti));
+      asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x90" : "+v"(eq) : "v"(r[i]), "v"(ti));
+    } else {
+      asm("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x8e" : "+v"(lt) : "v"(r[i]), "s"(ti));
+      asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x90" : "+v"(eq) : "v"(r[i]), "s"(ti));
+    }
   }
   F |= U & lt;
   U = eq;
@@ -287,11 +302,61 @@ __device__ __forceinline__ void noise_head(const GenArgs& a, uint2 own, uint32_t
 // (8 planes) of the i-th pair and the result goes back to the owner.  seq(l): the
 // (counter word 1, counter word 2) = (seq_lo, ctr_hi(seq, noise)) of lane l's sequence,
 // for the slot lanes.
-template <typename Seq>
+template <bool kSplit, typename Seq>
 __device__ __forceinline__ void noise_exchange(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
                                                uint32_t (&U)[4], uint32_t (&F)[4]) {
   const uint32_t t = a.thr_lo, lane = lane_id();
   const uint32_t nslots = a.slots - 1u < 64u ? a.slots : 64u;   // 1..64: every round makes progress
+  if constexpr (kSplit) {
+  // Split form: the two blocks (8 planes) of a pair go to two slot lanes, which compute
+  // one block each at the same time; a slot compares its planes for every bit (U = ~0)
+  // and returns (below, equal) masks, which the owner applies in plane order.  A round
+  // then takes one block's time for up to 32 pairs instead of two blocks' for 64, and
+  // the ~28 pairs after planes 1-8 of four words nearly always fit one round: ~2.3
+  // instead of ~2.56 blocks of wave time per word.
+  const uint32_t npr = nslots > 1u ? nslots >> 1 : 1u;   // pairs per round
+#pragma nounroll
+  for (uint32_t j = 2; j < (uint32_t)kNoiseBlocksPerWord; j += 2) {
+    uint32_t slot[4], tot = 0u;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint64_t b = __ballot(U[g] != 0u);
+      slot[g] = tot + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+      tot += (uint32_t)__builtin_popcountll(b);
+    }
+    if (tot == 0u) break;   // every bit of every pair decided
+#pragma nounroll
+    for (uint32_t s0 = 0; s0 < tot; s0 += npr) {   // rounds of 32 pairs (nearly always one)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (U[g] != 0u && slot[g] - s0 < npr) sm[slot[g] - s0] = lane | (uint32_t)g << 6;
+      wave_lds_sync();
+      const uint32_t pi = lane >> 1;
+      if (pi < npr && s0 + pi < tot) {
+        // (the read of sm[pi] returns before this lane's writes below: they depend on it)
+        const uint32_t mm = sm[pi], src = mm & 63u, w = w4 + (mm >> 6), blk = j + (lane & 1u);
+        const uint32_t k0 = a.k0, k1 = a.k1;
+        const uint2 sq = seq(src);
+        uint32_t xv[1][4] = {{w * kNoiseBlocksPerWord + blk, sq.x, sq.y, a.tag}};
+        philox_blocks<1>(xv, k0, k1);
+        uint32_t eq = ~0u, lt = 0u;
+        noise_planes4<true>(t >> (28u - 4u * blk), xv[0][0], xv[0][1], xv[0][2], xv[0][3], eq, lt);
+        su[lane] = lt; sm[lane] = eq;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int g = 0; g < 4; ++g)   // owners: planes 4j+1.. then 4j+5.., most significant first
+        if (U[g] != 0u && slot[g] - s0 < npr) {
+          const uint32_t s = 2u * (slot[g] - s0);
+          F[g] |= U[g] & su[s];
+          U[g] &= sm[s];
+          F[g] |= U[g] & su[s + 1];
+          U[g] &= sm[s + 1];
+        }
+      wave_lds_sync();
+    }
+  }
+  } else {
 #pragma nounroll
   for (uint32_t j = 2; j < (uint32_t)kNoiseBlocksPerWord; j += 2) {
     uint32_t slot[4], tot = 0u;
@@ -332,6 +397,7 @@ __device__ __forceinline__ void noise_exchange(const GenArgs& a, uint32_t* su, u
       wave_lds_sync();
     }
   }
+  }
 }
 
 // Flip masks F[g] of the words w4 + g (g < 4) of every lane's sequence, noise_word's
@@ -351,7 +417,7 @@ __device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, uint32_t* su,
   const uint2 own = seq(lane_id());
 #pragma unroll
   for (int g = 0; g < 4; ++g) noise_head(a, own, w4 + g, live[g], valid, U[g], F[g]);
-  noise_exchange(a, su, sm, seq, w4, U, F);
+  noise_exchange<CVD_GEN_XCHG_SPLIT>(a, su, sm, seq, w4, U, F);
 }
 
 // Encoder of one sequence, one received word at a time (bit-parallel, see above):
@@ -585,7 +651,7 @@ struct ChunkEncoder {
 #pragma unroll
       for (int g = 0; g < 4; ++g) F[g] = kValid;
     } else if (a->thr_lo) {
-      noise_exchange(*a, su, sm, seq, (uint32_t)w4, U, F);
+      noise_exchange<CVD_FUSED_XCHG_SPLIT>(*a, su, sm, seq, (uint32_t)w4, U, F);
     } else {
 #pragma unroll
       for (int g = 0; g < 4; ++g) F[g] = 0u;
