@@ -60,7 +60,7 @@ def test_tap_lists_equal_loop_generic_oracle(pkg, k, n, m, nt, taps, monkeypatch
 
 @pytest.mark.parametrize("gen1,gen2", [
     ([[[1, 1, 1]], [[1, 0, 1]]], [[[1, 0, 1]], [[1, 1, 1]]]),                       # m2: 3 taps -> kT 3
-    ([[[1, 0, 0, 1, 1]], [[1, 1, 1, 0, 1]]], [[[1, 1, 1, 0, 1]], [[1, 0, 0, 1, 1]]]),   # (23, 35): 4 -> kT 5
+    ([[[1, 1, 0, 1]], [[1, 1, 1, 1]]], [[[1, 1, 1, 1]], [[1, 1, 0, 1]]]),             # (15, 17): 4 -> kT 5
 ])
 def test_fused_tap_lists_equal_loop(pkg, gen1, gen2, monkeypatch):
     m = len(gen1[0][0]) - 1
