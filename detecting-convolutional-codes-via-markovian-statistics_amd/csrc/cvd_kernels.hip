@@ -52,6 +52,9 @@ namespace {
 #ifndef CVD_GEN_XCHG_SPLIT
 #define CVD_GEN_XCHG_SPLIT 1
 #endif
+#ifndef CVD_GEN_SEQ_LDS       // slot lanes read the sequence ids from LDS (1) or compute them (0)
+#define CVD_GEN_SEQ_LDS 0
+#endif
 #ifndef CVD_FUSED_XCHG_SPLIT   // the same in the fused trial kernel (ChunkEncoder::finish)
 #define CVD_FUSED_XCHG_SPLIT 0
 #endif
@@ -671,12 +674,30 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
   const bool lane_ok = li < a.count;
   const int64_t q = a.q0 + li;
   const uint64_t sid = (uint64_t)(a.seq_base + li * a.seq_stride);
+#if CVD_GEN_SEQ_LDS
   __shared__ NoiseLds noise_lds[kBlock / 64];
   NoiseLds& nl = noise_lds[threadIdx.x / 64];
   nl.slo[lane_id()] = (uint32_t)sid;
   nl.nhi[lane_id()] = ctr_hi(sid, kKindNoise);
   wave_lds_sync();
   auto seq = [&](uint32_t l) { return make_uint2(nl.slo[l], nl.nhi[l]); };
+  uint32_t* const su = nl.u;
+  uint32_t* const sm = nl.m;
+#else
+  // the slot lanes' sequence ids from the lane index (one 64-bit multiply-add), so
+  // that a block holds 2 KB of LDS: five generator blocks fit beside a rate-2/3
+  // detector block (141 KB of a CU's 160 KB) instead of four
+  __shared__ uint32_t xchg[kBlock / 64][128];
+  uint32_t* const su = xchg[threadIdx.x / 64];
+  uint32_t* const sm = su + 64;
+  // (wave-uniform: the wave's first lane's sequence id s0 and the stride in SGPRs)
+  const int64_t li0 = (int64_t)blockIdx.x * kBlock + (int64_t)__builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+  const uint64_t s0 = (uint64_t)(a.seq_base + li0 * a.seq_stride), sstr = (uint64_t)a.seq_stride;
+  auto seq = [&](uint32_t l) {
+    const uint64_t s = s0 + (uint64_t)l * sstr;
+    return make_uint2((uint32_t)s, ctr_hi(s, kKindNoise));
+  };
+#endif
   const int64_t nwords = (a.N + SPW - 1) / SPW;
   const int64_t nw4 = (nwords + 3) & ~(int64_t)3;
   ChunkEncoder<k, n, kT> enc;
@@ -692,7 +713,7 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) live[g] = lane_ok && w4 + g < nwords;
     uint32_t out4[4];
-    enc.chunk(nl.u, nl.m, seq, w4, live, nwords, out4);
+    enc.chunk(su, sm, seq, w4, live, nwords, out4);
     if (lane_ok)
       *reinterpret_cast<uint4*>(a.r + chunk_index(w4 >> 2, a.pitch, q)) = make_uint4(out4[0], out4[1], out4[2], out4[3]);
   }
