@@ -305,18 +305,65 @@ __device__ __forceinline__ void noise_head(const GenArgs& a, uint2 own, uint32_t
 // (8 planes) of the i-th pair and the result goes back to the owner.  seq(l): the
 // (counter word 1, counter word 2) = (seq_lo, ctr_hi(seq, noise)) of lane l's sequence,
 // for the slot lanes.
-template <bool kSplit, typename Seq>
-__device__ __forceinline__ void noise_exchange(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
-                                               uint32_t (&U)[4], uint32_t (&F)[4]) {
+template <typename Seq>
+__device__ __forceinline__ void noise_exchange_pair(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq,
+                                                    uint32_t w4, uint32_t (&U)[4], uint32_t (&F)[4]) {
   const uint32_t t = a.thr_lo, lane = lane_id();
   const uint32_t nslots = a.slots - 1u < 64u ? a.slots : 64u;   // 1..64: every round makes progress
-  if constexpr (kSplit) {
-  // Split form: the two blocks (8 planes) of a pair go to two slot lanes, which compute
-  // one block each at the same time; a slot compares its planes for every bit (U = ~0)
-  // and returns (below, equal) masks, which the owner applies in plane order.  A round
-  // then takes one block's time for up to 32 pairs instead of two blocks' for 64, and
-  // the ~28 pairs after planes 1-8 of four words nearly always fit one round: ~2.3
-  // instead of ~2.56 blocks of wave time per word.
+#pragma nounroll
+  for (uint32_t j = 2; j < (uint32_t)kNoiseBlocksPerWord; j += 2) {
+    uint32_t slot[4], tot = 0u;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint64_t b = __ballot(U[g] != 0u);
+      slot[g] = tot + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+      tot += (uint32_t)__builtin_popcountll(b);
+    }
+    if (tot == 0u) break;   // every bit of every pair decided
+#pragma nounroll
+    for (uint32_t s0 = 0; s0 < tot; s0 += nslots) {   // rounds of 64 slots (nearly always one)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (U[g] != 0u && slot[g] - s0 < nslots) { su[slot[g] - s0] = U[g]; sm[slot[g] - s0] = lane | (uint32_t)g << 6; }
+      wave_lds_sync();
+      const bool busy = lane < nslots && s0 + lane < tot;
+      if (busy) {
+        uint32_t Un = su[lane], Fn = 0u;
+        const uint32_t mm = sm[lane], src = mm & 63u, w = w4 + (mm >> 6);
+        const uint32_t k0 = a.k0, k1 = a.k1;
+        const uint2 sq = seq(src);
+        uint32_t xv[2][4];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          xv[b][0] = w * kNoiseBlocksPerWord + j + (uint32_t)b;
+          xv[b][1] = sq.x; xv[b][2] = sq.y; xv[b][3] = a.tag;
+        }
+        philox_blocks<2>(xv, k0, k1);
+        noise_planes4(t >> (28u - 4u * j), xv[0][0], xv[0][1], xv[0][2], xv[0][3], Un, Fn);
+        noise_planes4(t >> (24u - 4u * j), xv[1][0], xv[1][1], xv[1][2], xv[1][3], Un, Fn);
+        su[lane] = Un; sm[lane] = Fn;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int g = 0; g < 4; ++g)   // owners (U still holds the value they sent)
+        if (U[g] != 0u && slot[g] - s0 < nslots) { U[g] = su[slot[g] - s0]; F[g] |= sm[slot[g] - s0]; }
+      wave_lds_sync();
+    }
+  }
+}
+
+// Split form: the two blocks (8 planes) of a pair go to two slot lanes, which compute
+// one block each at the same time; a slot compares its planes for every bit (U = ~0)
+// and returns (below, equal) masks, which the owner applies in plane order.  A round
+// takes one block's time for up to 32 pairs instead of two blocks' for 64 (the ~28
+// pairs left after planes 1-8 of four words nearly always fit one round).  Measured:
+// the generator alone 1% faster, the fused kernel (4 more VGPRs) slower
+// (profiles/r04n); so the generator uses it and the fused kernel does not.
+template <typename Seq>
+__device__ __forceinline__ void noise_exchange_split(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq,
+                                                     uint32_t w4, uint32_t (&U)[4], uint32_t (&F)[4]) {
+  const uint32_t t = a.thr_lo, lane = lane_id();
+  const uint32_t nslots = a.slots - 1u < 64u ? a.slots : 64u;
   const uint32_t npr = nslots > 1u ? nslots >> 1 : 1u;   // pairs per round
 #pragma nounroll
   for (uint32_t j = 2; j < (uint32_t)kNoiseBlocksPerWord; j += 2) {
@@ -359,48 +406,13 @@ __device__ __forceinline__ void noise_exchange(const GenArgs& a, uint32_t* su, u
       wave_lds_sync();
     }
   }
-  } else {
-#pragma nounroll
-  for (uint32_t j = 2; j < (uint32_t)kNoiseBlocksPerWord; j += 2) {
-    uint32_t slot[4], tot = 0u;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const uint64_t b = __ballot(U[g] != 0u);
-      slot[g] = tot + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-      tot += (uint32_t)__builtin_popcountll(b);
-    }
-    if (tot == 0u) break;   // every bit of every pair decided
-#pragma nounroll
-    for (uint32_t s0 = 0; s0 < tot; s0 += nslots) {   // rounds of 64 slots (nearly always one)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        if (U[g] != 0u && slot[g] - s0 < nslots) { su[slot[g] - s0] = U[g]; sm[slot[g] - s0] = lane | (uint32_t)g << 6; }
-      wave_lds_sync();
-      const bool busy = lane < nslots && s0 + lane < tot;
-      if (busy) {
-        uint32_t Un = su[lane], Fn = 0u;
-        const uint32_t mm = sm[lane], src = mm & 63u, w = w4 + (mm >> 6);
-        const uint32_t k0 = a.k0, k1 = a.k1;
-        const uint2 sq = seq(src);
-        uint32_t xv[2][4];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          xv[b][0] = w * kNoiseBlocksPerWord + j + (uint32_t)b;
-          xv[b][1] = sq.x; xv[b][2] = sq.y; xv[b][3] = a.tag;
-        }
-        philox_blocks<2>(xv, k0, k1);
-        noise_planes4(t >> (28u - 4u * j), xv[0][0], xv[0][1], xv[0][2], xv[0][3], Un, Fn);
-        noise_planes4(t >> (24u - 4u * j), xv[1][0], xv[1][1], xv[1][2], xv[1][3], Un, Fn);
-        su[lane] = Un; sm[lane] = Fn;
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int g = 0; g < 4; ++g)   // owners (U still holds the value they sent)
-        if (U[g] != 0u && slot[g] - s0 < nslots) { U[g] = su[slot[g] - s0]; F[g] |= sm[slot[g] - s0]; }
-      wave_lds_sync();
-    }
-  }
-  }
+}
+
+template <bool kSplit, typename Seq>
+__device__ __forceinline__ void noise_exchange(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
+                                               uint32_t (&U)[4], uint32_t (&F)[4]) {
+  if constexpr (kSplit) noise_exchange_split(a, su, sm, seq, w4, U, F);
+  else noise_exchange_pair(a, su, sm, seq, w4, U, F);
 }
 
 // Flip masks F[g] of the words w4 + g (g < 4) of every lane's sequence, noise_word's
