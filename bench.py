@@ -107,8 +107,6 @@ def parse():
                     help="markov: the relative-Viterbi-metric detector (headline); parity: the "
                          "parity-template baseline of comp_parity.py on the same streams")
     ap.add_argument("--gamma", type=float, default=0.6, help="parity baseline threshold (comp_parity.py:151)")
-    ap.add_argument("--gen-priority", type=int, default=0,
-                    help="HIP stream priority of the overlapped generator stream (-1: high)")
     ap.add_argument("--overlap", type=int, default=-1,
                     help="generate the next batch on a second stream while the detector runs "
                          "(-1: auto = on for the table automaton, where it measured faster)")
@@ -264,7 +262,7 @@ def main():
     bufs = [det.stream_buffer(N, 2 * B) for _ in range(nbuf)]
     counts = torch.zeros((npg, 2), dtype=torch.int64, device=det.device)
     main = torch.cuda.current_stream()
-    gstream = torch.cuda.Stream(device=det.device, priority=a.gen_priority) if a.overlap else main
+    gstream = torch.cuda.Stream(device=det.device) if a.overlap else main
     use_multi = sweep_all and bool(a.multi) and not (a.overlap or a.fused or parity)
     groups = (det.multi_groups([models[p] for p in p_grid]) if use_multi
               else [[j] for j in range(per_step)])      # positions within a step's units

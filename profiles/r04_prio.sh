@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: C3 with the overlapped generator stream at high HIP priority (--gen-priority -1)
+# Round 4 (option since removed from bench.py): C3 with the overlapped generator stream at high HIP priority (--gen-priority -1)
 set -uo pipefail
 OUT=$1; shift
 mkdir -p $OUT
