@@ -229,6 +229,91 @@ extern "C" __global__ __launch_bounds__(256) void bitslice_acs_asm(Masks mk, int
   }
 }
 
+// Third form: the step minimum known BEFORE the ACS.  A normalised vector has a zero
+// state, whose better branch costs min(e, 2 - e) <= 1, so the new minimum mu is 0 or 1,
+// and 0 exactly when some zero state has e in {0, 2} (bit 0 of e clear).  The ACS then
+// adds E - mu in 4-bit two's complement (every candidate stays >= 0) and needs no
+// normalisation pass.
+__device__ __forceinline__ void add4s(const uint32_t (&d)[W], uint32_t b0, uint32_t b1, uint32_t b23,
+                                      uint32_t (&s)[W]) {
+  s[0] = d[0] ^ b0;
+  uint32_t c = d[0] & b0, c1, c2;
+  BOP3(s[1], d[1], b1, c, 0x96);
+  BOP3(c1, d[1], b1, c, 0xe8);
+  BOP3(s[2], d[2], b23, c1, 0x96);
+  BOP3(c2, d[2], b23, c1, 0xe8);
+  BOP3(s[3], d[3], b23, c2, 0x96);
+}
+
+template <int PH>
+__device__ __forceinline__ void stepb(uint32_t (&R)[2][W], uint32_t y, const Masks& mk, uint32_t& musum) {
+  constexpr int L5tab[6] = {0, 5, 4, 3, 2, 1};
+  constexpr int L5 = L5tab[PH];
+  const uint32_t Y0 = 0u - (y & 1u), Y1 = 0u - ((y >> 1) & 1u);
+  uint32_t e0[2], e1[2], ez[2], hit = 0u;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const uint32_t d0 = mk.o0[PH][r] ^ Y0, o1 = mk.o1[PH][r];
+    BOP3(e0[r], d0, o1, Y1, 0x96);      // bit 0 of e
+    BOP3(e1[r], d0, o1, Y1, 0x60);      // bit 1 of e (e == 2)
+    BOP3(ez[r], d0, o1, Y1, 0x09);      // e == 0
+    uint32_t t, z;
+    asm("v_or3_b32 %0, %1, %2, %3" : "=v"(t) : "v"(R[r][0]), "v"(R[r][1]), "v"(R[r][2]));
+    BOP3(z, t, R[r][3], e0[r], 0x01);   // zero state with e in {0, 2}: ~t & ~d3 & ~e0
+    hit |= z;
+  }
+  const uint32_t M = hit ? 0u : ~0u;    // mu = 1 on every position
+  musum += hit ? 0u : 1u;
+  uint32_t N[2][W];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    uint32_t P[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      if constexpr (L5 == 0) P[i] = R[1 - r][i];
+      else P[i] = flipa<L5 - 1>(R[r][i]);
+    }
+    // own branch e - mu, partner branch (2 - e) - mu, as 4-bit two's complement planes
+    const uint32_t b0 = e0[r] ^ M;
+    uint32_t a1, p1;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(a1) : "v"(M), "v"(ez[r]), "v"(e1[r]));   // M ? (e == 0) : e1
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(p1) : "v"(M), "v"(e1[r]), "v"(ez[r]));   // M ? (e == 2) : (e == 0)
+    const uint32_t a23 = M & ez[r], p23 = M & e1[r];
+    uint32_t a[W], b[W];
+    add4s(R[r], b0, a1, a23, a);
+    add4s(P, b0, p1, p23, b);
+    min4a(a, b, N[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < W; ++i) R[r][i] = N[r][i];
+}
+
+extern "C" __global__ __launch_bounds__(256) void bitslice_acs_mu(Masks mk, int64_t nsix, uint32_t seed,
+                                                                  uint32_t* out, int64_t nlanes) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t R[2][W] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+  uint32_t s = seed ^ (uint32_t)(q * 0x9E3779B9u), musum = 0u;
+  if (s == 0u) s = 1u;
+  for (int64_t t = 0; t < nsix; ++t) {
+    uint32_t w = xs(s);
+    stepb<0>(R, w & 3u, mk, musum);
+    stepb<1>(R, (w >> 2) & 3u, mk, musum);
+    stepb<2>(R, (w >> 4) & 3u, mk, musum);
+    stepb<3>(R, (w >> 6) & 3u, mk, musum);
+    stepb<4>(R, (w >> 8) & 3u, mk, musum);
+    stepb<5>(R, (w >> 10) & 3u, mk, musum);
+  }
+  if (q < nlanes) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < W; ++i) out[q * 9 + r * W + i] = R[r][i];
+    out[q * 9 + 8] = musum;
+  }
+}
+
 // host launcher (ctypes): masks = o0[6][2] then o1[6][2]; returns the kernel's ms
 extern "C" int bitslice_run(const uint32_t* masks, int64_t nsix, uint32_t seed, uint32_t* d_out, int64_t nlanes,
                             float* ms_out, int variant) {
@@ -242,7 +327,8 @@ extern "C" int bitslice_run(const uint32_t* masks, int64_t nsix, uint32_t seed, 
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -1;
   const unsigned grid = (unsigned)((nlanes + 255) / 256);
   hipEventRecord(e0, nullptr);
-  if (variant) hipLaunchKernelGGL(bitslice_acs_asm, dim3(grid), dim3(256), 0, nullptr, mk, nsix, seed, d_out, nlanes);
+  if (variant == 2) hipLaunchKernelGGL(bitslice_acs_mu, dim3(grid), dim3(256), 0, nullptr, mk, nsix, seed, d_out, nlanes);
+  else if (variant) hipLaunchKernelGGL(bitslice_acs_asm, dim3(grid), dim3(256), 0, nullptr, mk, nsix, seed, d_out, nlanes);
   else hipLaunchKernelGGL(bitslice_acs, dim3(grid), dim3(256), 0, nullptr, mk, nsix, seed, d_out, nlanes);
   hipEventRecord(e1, nullptr);
   if (hipEventSynchronize(e1) != hipSuccess) return -2;

@@ -78,7 +78,7 @@ def main():
     out_sym, nxt = R.encoder_tables(g1, 6, 1, 2)
     mk = masks(out_sym)
     res = {}
-    for variant, vname in ((0, "compiler"), (1, "bitop3_asm")):
+    for variant, vname in ((0, "compiler"), (1, "bitop3_asm"), (2, "mu_first")):
         for tag, ns, nl in (("check", 50, 256), ("warm", nsix, lanes), ("time", nsix, lanes)):
             out = torch.zeros(nl * 9, dtype=torch.int32, device="cuda")
             ms = ctypes.c_float(0.0)
