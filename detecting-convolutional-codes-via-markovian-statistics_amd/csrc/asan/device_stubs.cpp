@@ -14,6 +14,7 @@ int cvd::explicit_kernel_of(const cvd_model& M) { return M.k1b_ok ? CVD_KERNEL_B
 bool cvd::mc_fused_preferred(const cvd_model&) { return false; }
 bool cvd::walk_preferred(const cvd_model&, bool) { return false; }
 bool cvd::ldsf_preferred(const cvd_model&) { return false; }
+int64_t cvd::multi_variant(const cvd_model&) { return 0; }
 int cvd::device_learn_sparse(const CodeDesc&, int64_t, int64_t, uint64_t, double, int, void*, std::vector<uint8_t>&,
                              std::vector<int64_t>&, int64_t&, LearnStats*) {
   cvd::set_error("no device in the host sanitizer build");

@@ -18,6 +18,7 @@ typedef unsigned long long uint64_t;
 typedef __SIZE_TYPE__ size_t;
 #endif
 #include "cvd_keys.h"
+#include "cvd_bitslice.h"
 
 namespace cvd_dev {
 
@@ -1224,3 +1225,6 @@ __device__ __forceinline__ void k1b_multi(const MultiArgs& ma) {
 }
 
 }  // namespace cvd_dev
+
+// the bit-sliced m = 6 kernel (k1s) and the specialised entries
+#include "cvd_k1s.h"

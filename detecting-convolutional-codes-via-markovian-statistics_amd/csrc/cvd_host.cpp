@@ -28,6 +28,7 @@
 
 #include "../../include/cvd.h"
 #include "cvd_internal.h"
+#include "cvd_bitslice.h"
 
 using namespace cvd;
 
@@ -599,6 +600,61 @@ void build_hash(cvd_model& Mo) {
     std::memcpy(hw, dw, sizeof(uint32_t) * Mo.h_rsw);
   });
   Mo.slot0 = (int32_t)dev_of[0];   // D_0 = 0 is row 0 in both model kinds
+  // Bit-sliced tables of the m = 6 kernel k1s (cvd_bitslice.h): the same rows and records,
+  // found by the hash of the canonical digest plane z = bit0(D) ^ bit1(D) (one filter entry
+  // per row whatever the lane's layout phase); a directory slot holds the row's image at
+  // each of the six phases (the exact compare) and its record; a.dkey the six images by
+  // device row id (walk mode).  Load <= 1/8 by default (CVD_BS_LOAD_LOG2): 256-B slots, so
+  // the directory stays within 2 GiB at 10^6 rows; offsets into it are 64-bit.
+  Mo.bs = bitslice_preferred(Mo);
+  Mo.h_bfilt.clear(); Mo.h_bfilt_lds.clear(); Mo.h_bkey.clear(); Mo.h_bdkey.clear();
+  Mo.bhcap = 0; Mo.bmax_probe = 0;
+  if (Mo.bs) {
+    int bload = 3;
+    if (const char* e = std::getenv("CVD_BS_LOAD_LOG2")) bload = std::max(1, std::min(5, std::atoi(e)));
+    int64_t bcap = 64;
+    while (bcap < ((int64_t)1 << bload) * Mo.n_rows) bcap <<= 1;
+    Mo.bhcap = bcap;
+    constexpr int kSlotW = 64, kRecW = 48, kImgW = 48;
+    Mo.h_bkey.assign((size_t)bcap * kSlotW, 0u);   // c = 0 in every record: empty
+    Mo.h_bfilt.assign((size_t)fcap, 0u);
+    Mo.h_bfilt_lds.assign(ldsf ? (size_t)fcap : 0u, 0u);
+    Mo.h_bdkey.assign((size_t)Mo.n_rows * kImgW, 0u);
+    std::vector<uint32_t> bph((size_t)Mo.n_rows), bpl((size_t)Mo.n_rows);
+    parallel_for(Mo.n_rows, [&](int64_t i, int) {
+      uint32_t z[2];
+      bs_digest(Mo.keys.data() + (size_t)i * M, z);
+      key_hash(z, 2, bph[(size_t)i], bpl[(size_t)i]);
+    });
+    std::vector<uint8_t> used((size_t)bcap, 0);
+    std::vector<int64_t> bslot((size_t)Mo.n_rows);
+    for (int64_t i = 0; i < Mo.n_rows; ++i) {
+      const uint32_t ph = bph[(size_t)i], pl = bpl[(size_t)i];
+      const size_t fb = (size_t)filter_block_index(pl, (uint32_t)(fcap / 2 - 1));
+      Mo.h_bfilt[2 * fb] |= filter_pattern(filter_pattern_index(ph, npat));
+      Mo.h_bfilt[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph, npat), npat);
+      if (ldsf) {
+        const unsigned nl = 1u << kFilterPatBitsLds;
+        Mo.h_bfilt_lds[2 * fb] |= filter_pattern(filter_pattern_index(ph, nl));
+        Mo.h_bfilt_lds[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph, nl), nl);
+      }
+      uint64_t slot = ph & (uint64_t)(bcap - 1);
+      int probe = 0;
+      while (used[slot]) { slot = (slot + 1) & (uint64_t)(bcap - 1); ++probe; }
+      used[slot] = 1;
+      Mo.bmax_probe = std::max(Mo.bmax_probe, probe);
+      bslot[(size_t)i] = (int64_t)slot;
+    }
+    parallel_for(Mo.n_rows, [&](int64_t i, int) {
+      uint32_t* sp = Mo.h_bkey.data() + (size_t)bslot[(size_t)i] * kSlotW;
+      uint32_t* dk = Mo.h_bdkey.data() + (size_t)dev_of[(size_t)i] * kImgW;
+      for (int ph = 0; ph < 6; ++ph) {
+        bs_image(Mo.keys.data() + (size_t)i * M, ph, sp + 8 * ph);
+        std::memcpy(dk + 8 * ph, sp + 8 * ph, 8 * sizeof(uint32_t));
+      }
+      std::memcpy(sp + kRecW, Mo.h_drow.data() + (size_t)dev_of[(size_t)i] * Mo.h_rsw, sizeof(uint32_t) * 16);
+    });
+  }
   // two-step walk records (k1b_walk), for models that walk: per device row d and word pair
   // (r1, r2), 32 B {log P̂1(d, r1), log P̂1(d1, r2), (d1 + 1) | c(d, r1) << 28,
   // (d2 + 1) | c(d1, r2) << 28}, d1 / d2 the rows after one / two steps (0 = not a row)
@@ -702,6 +758,12 @@ void build_bmp(cvd_model& Mo, const Tabs& T) {
 }
 
 }  // namespace
+
+bool cvd::bitslice_preferred(const cvd_model& M) {
+  const char* e = std::getenv("CVD_BITSLICE");
+  if (e && e[0] == '0') return false;
+  return M.k1b_ok && M.dec.k == 1 && M.dec.n == 2 && M.dec.m == 6;
+}
 
 bool cvd::explicit_supported(int m, int k, int n) {
   // nibble storage of un-normalised metrics: D <= ceil(m/k)*n, plus one branch (<= n)
@@ -916,8 +978,8 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
     return rc;
   }
   if (explicit_supported(T.m, T.k, T.n)) {
+    build_bmp(*Mo, T);   // (first: the butterfly check decides the bit-sliced tables)
     build_hash(*Mo);
-    build_bmp(*Mo, T);
     pt.mark("row table");
   }
   *out = Mo.release();
@@ -1049,8 +1111,8 @@ extern "C" int cvd_model_load(const char* path, cvd_model** out) {
   }
   if (explicit_supported(d.m, d.k, d.n)) {
     Tabs T = make_tabs(Mo->dec);
-    build_hash(*Mo);
     build_bmp(*Mo, T);
+    build_hash(*Mo);
   }
   *out = Mo.release();
   return CVD_OK;
@@ -1099,6 +1161,8 @@ extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
   info->walk = Mo->k1b_ok && Mo->hcap > 0 && walk_preferred(*Mo) && (Mo->device < 0 || Mo->rtc_fn) ? 1 : 0;
   info->lds_filter = Mo->device >= 0 ? (Mo->rtc_fn && Mo->rtc_ldsf ? 1 : 0)
                                      : (Mo->k1b_ok && Mo->hcap > 0 && ldsf_preferred(*Mo) ? 1 : 0);
+  info->pad0 = 0;
+  info->multi_variant = multi_variant(*Mo);
   return CVD_OK;
 }
 

@@ -45,6 +45,17 @@ struct cvd_model {
                                   // dword 3 of entry r = the T_ref count c(r)
   std::vector<uint32_t> h_dkey;   // [n_rows][NW]: row keys (device layout) by device row id
   std::vector<uint32_t> h_t2;     // [n_rows][16][8]: two-step walk records (walking models only)
+  // bit-sliced tables of the m = 6 kernel k1s (cvd_bitslice.h, cvd_k1s.h), beside the nibble
+  // ones (which the other kernels and the trace path read): the Bloom filter over the
+  // canonical digest hash, the directory of 256-B slots {six phase images, record}, and six
+  // images per row by device row id
+  bool bs = false;
+  int64_t bhcap = 0;
+  int32_t bmax_probe = 0;
+  std::vector<uint32_t> h_bfilt, h_bfilt_lds;   // [fcap] each (the LDS copy only with h_filt_lds)
+  std::vector<uint32_t> h_bkey;   // [bhcap][64]: images 8 words x 6 phases, records 4 x 4 (c = 0: empty)
+  std::vector<uint32_t> h_bdkey;  // [n_rows][48]
+  bool rtc_bs = false;            // the specialised kernel built for this model is k1s
   int32_t slot0 = 0;              // row of D_0 = 0 (always 0)
   std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
   // k = 1 orbit kernel: successor(r ^ g0) = successor(r) with states 2j <-> 2j+1 swapped,
@@ -77,6 +88,10 @@ struct cvd_model {
   uint32_t* d_drow = nullptr;
   uint32_t* d_dkey = nullptr;
   uint32_t* d_t2 = nullptr;
+  uint32_t* d_bfilt = nullptr;
+  uint32_t* d_bfilt_lds = nullptr;
+  uint32_t* d_bkey = nullptr;
+  uint32_t* d_bdkey = nullptr;
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
   uint32_t* d_bfly = nullptr;
@@ -131,6 +146,11 @@ int rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, v
                      void** fn_multi_out = nullptr);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);
+// the model gets the bit-sliced tables and kernel (m = 6 standard-butterfly codes;
+// CVD_BITSLICE=0 turns it off)
+bool bitslice_preferred(const cvd_model& M);
+// id of the multi-model launch variant (cvd_model_info.multi_variant; cvd_kernels.hip)
+int64_t multi_variant(const cvd_model& M);
 
 // P̂1 learning chain on the GPU (cvd_learn.hip): identical outputs to the host chain.
 struct LearnStats {

@@ -1,0 +1,499 @@
+// The m = 6 bit-sliced detector k1s (the JIT's CVD_K1B_BITSLICE=1 variant of the
+// code-specialised kernel, cvd_rtc.cpp).  Included at the end of cvd_device.h (whose
+// ExpArgs, filter patterns, walk-mode constants and helpers it uses); the run-time compile
+// embeds it after that file.
+//
+// The detector of k1b_body / k1b_walk, sums identical bit for bit, with the 64 metrics as
+// four bit-planes of two words in the rotating layout of cvd_bitslice.h.
+// Per step: the branch-metric planes of (phase, y) from an LDS table, mu first, the ACS of
+// both words (own and partner adds, a borrow-chain min), the T_ref count off the partner
+// planes and, for a lane whose new vector must be hashed, the canonical digest hash.  The
+// row tables are the bit-sliced ones (cvd_host.cpp build_hash with bs): the Bloom filter
+// over the digest hash, 256-byte directory slots {six phase images, the row's record}, six
+// images per learned row by row id (walk mode) and the usual dense records.  The layout
+// phase is compile-time in the lockstep loop (six steps per iteration) and wave-uniform in
+// walk mode.
+#pragma once
+
+#ifndef CVD_K1B_BITSLICE
+#define CVD_K1B_BITSLICE 0
+#endif
+
+namespace cvd_dev {
+
+constexpr int kBsSlotShift = 6;      // directory slot: 64 dwords
+constexpr int kBsRecWord = 48;       // record r at dwords 48 + 4 r of a slot (images 8 x 6 before it)
+constexpr int kBsDkeyWords = 48;     // six images per row in a.dkey
+constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
+
+// LDS: per (phase, y) two uint4 {e0, e1, ez, 0} of word 0 and word 1 (cvd::bs_eplanes)
+__device__ __forceinline__ uint4* bs_etab_lds() {
+  __shared__ uint4 s_et[6 * 4 * 2];
+  return s_et;
+}
+template <uint64_t XM>
+__device__ __forceinline__ void fill_bs_etab() {
+  uint4* t = bs_etab_lds();
+  for (int i = threadIdx.x; i < 24; i += blockDim.x) {
+    const cvd::BsE E = cvd::bs_eplanes(XM, i >> 2, (uint32_t)(i & 3));
+    t[2 * i] = make_uint4(E.e0[0], E.e1[0], E.ez[0], 0u);
+    t[2 * i + 1] = make_uint4(E.e0[1], E.e1[1], E.ez[1], 0u);
+  }
+}
+
+// P̂1 row cursor over the bit-sliced tables (RowCursor's protocol: slot >= 0 known row id,
+// -1 known unvisited row, -2 pending hash probe)
+struct BsCursor {
+  int32_t slot, pnx;
+  uint32_t hs, fb, fw, fb1, fw1, pc;
+  bool cand;
+  double plp;
+  uint32_t pkey[8];
+  // entry rn (16 B {log P̂1, successor row, T_ref count c}) of learned row s, dense records
+  __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
+    uint32_t o;
+    asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o) : "v"(rn), "v"((uint32_t)s * 64u));
+    const uint4 v = ld_off<uint4>(a.drow, o);
+    pc = v.w;
+    pnx = (int32_t)v.z;
+    plp = __hiloint2double((int)v.y, (int)v.x);
+  }
+  __device__ void start(const ExpArgs& a, uint32_t r0) {
+    slot = a.slot0; hs = 0u; fb = 0u; fw = 0u; fb1 = 0u; fw1 = 0u; cand = false; pc = 1u;
+    prefetch_row(a, slot, r0);
+  }
+  // ordering fences (RowCursor::fence): the waits for the loads issued a step / half a step
+  // earlier land after the ACS work the dependency names
+  __device__ void fence(uint32_t dep) {
+    asm volatile("" : "+v"(fw), "+v"(fw1), "+v"(slot), "+v"(pnx), "+v"(plp) : "v"(dep));
+  }
+  __device__ void fence_keys(uint32_t dep) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
+    asm volatile("" : "+v"(pc) : "v"(dep));
+  }
+  __device__ static const uint32_t* slot_ptr(const ExpArgs& a, uint32_t s) {
+    return a.hkey + ((size_t)s << kBsSlotShift);
+  }
+  __device__ static void load_image(const uint32_t* p, uint32_t (&k)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p), v = *reinterpret_cast<const uint4*>(p + 4);
+    k[0] = u.x; k[1] = u.y; k[2] = u.z; k[3] = u.w; k[4] = v.x; k[5] = v.y; k[6] = v.z; k[7] = v.w;
+  }
+  // filter positive: the home slot's image of phase PH and its record for word r
+  template <int PH>
+  __device__ void mid(const ExpArgs& a, uint32_t r) {
+    cand = slot == -2 && ((fb & ~fw) | (fb1 & ~fw1)) == 0u;
+    if (cand) {
+      const uint32_t* sp = slot_ptr(a, hs);
+      load_image(sp + 8 * PH, pkey);
+      const uint4 v = *reinterpret_cast<const uint4*>(sp + kBsRecWord + 4u * r);
+      pc = v.w;
+      pnx = (int32_t)v.z;
+      plp = __hiloint2double((int)v.y, (int)v.x);
+    }
+  }
+  __device__ static bool same(const uint32_t (&k)[8], const uint32_t (&R)[2][4]) {
+    uint32_t d = k[0] ^ R[0][0];
+    d = cvd::bs_bop3<cvd::kTtXorOr>(k[1], R[0][1], d);
+    d = cvd::bs_bop3<cvd::kTtXorOr>(k[2], R[0][2], d);
+    d = cvd::bs_bop3<cvd::kTtXorOr>(k[3], R[0][3], d);
+    d = cvd::bs_bop3<cvd::kTtXorOr>(k[4], R[1][0], d);
+    d = cvd::bs_bop3<cvd::kTtXorOr>(k[5], R[1][1], d);
+    d = cvd::bs_bop3<cvd::kTtXorOr>(k[6], R[1][2], d);
+    d = cvd::bs_bop3<cvd::kTtXorOr>(k[7], R[1][3], d);
+    asm volatile("" : "+v"(d));
+    return d == 0u;
+  }
+  // log P̂1(row(D_{t-1}), r), D_{t-1} = planes R at phase PH; afterwards `slot` describes row(D_t)
+  template <int PH>
+  __device__ double resolve(const ExpArgs& a, const uint32_t (&R)[2][4], uint32_t r, double lpu) {
+    double lpv = lpu;
+    int32_t ns = -2;
+    if (slot >= 0) {
+      lpv = plp; ns = pnx;
+    } else if (cand) {
+      if (same(pkey, R)) {
+        lpv = plp; ns = pnx;
+      } else if (pc != 0u) {
+        // the home slot holds another row (an empty slot has c = 0): linear probing up to
+        // an empty slot
+        uint32_t sl = hs;
+        for (int pr = 1; pr <= a.max_probe; ++pr) {
+          sl = (sl + 1u) & a.hmask;
+          const uint32_t* sp = slot_ptr(a, sl);
+          const uint4 v = *reinterpret_cast<const uint4*>(sp + kBsRecWord + 4u * r);
+          if (v.w == 0u) break;
+          uint32_t k[8];
+          load_image(sp + 8 * PH, k);
+          if (same(k, R)) {
+            lpv = __hiloint2double((int)v.y, (int)v.x);
+            ns = (int32_t)v.z;
+            break;
+          }
+        }
+      }
+    }
+    slot = ns;
+    return lpv;
+  }
+  // D_t (planes N at phase PH) is known: issue the next step's loads (kRow: the dense
+  // record of a known row; walk mode loads its own)
+  template <int PH, bool kRow = true>
+  __device__ void prefetch(const ExpArgs& a, const uint32_t (&N)[2][4], uint32_t rn) {
+    if (slot >= 0) {
+      if (kRow) prefetch_row(a, slot, rn);
+    } else if (slot == -2) {
+      uint32_t ph, pl;
+      cvd::bs_digest_hash<PH>(N, ph, pl);
+      hs = ph & a.hmask;
+      const uint2 pp = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(filter_patterns_lds()) +
+                                                       (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 3)));
+      fb = pp.x;
+      fb1 = pp.y;
+#if CVD_K1B_LDSF
+      const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + (pl & a.fmask4));
+#else
+      const uint2 f = ld_off<uint2>(a.filt, pl & a.fmask4);
+#endif
+      fw = f.x;
+      fw1 = f.y;
+    }
+  }
+};
+
+// one bit-sliced step of a lane: D_{t-1} = R (phase PH) -> N (phase PH + 1) under word rr,
+// the filter-positive loads issued between the two words' ACS
+template <int PH, bool kUni>
+__device__ __forceinline__ void bs_step(const ExpArgs& a, BsCursor& cur, const uint32_t (&R)[2][4], uint32_t rr,
+                                        uint32_t (&N)[2][4], uint32_t& c) {
+  const uint4* et = bs_etab_lds() + (PH * 4 + rr) * 2;
+  const uint4 E0 = et[0], E1 = et[1];
+  const uint32_t e0[2] = {E0.x, E1.x}, e1[2] = {E0.y, E1.y}, ez[2] = {E0.z, E1.z};
+  uint32_t mu;
+  cvd::bs_step_core<PH, kUni>(R, e0, e1, ez, N, mu, c, [&](uint32_t dep) {
+    cur.fence(dep);                  // dep: the first word's ACS result
+    cur.template mid<PH>(a, rr);
+  });
+}
+
+// H1 waves in walk mode (k1b_walk's schedule; the planes' layout phase is the wave's)
+template <uint64_t XM>
+__device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64_t vmask, const double* s_lt) {
+  constexpr bool kUni = xm_uni<6, XM>();
+  if (CVD_WALK_ABL & 1) return;
+  const bool valid = qwave + lane_id() < a.nseq;
+  const uint32_t N = (uint32_t)a.N;
+  const uint32_t nwords = (N + 15u) / 16u;
+  const size_t cstride = (size_t)a.nseq * 4;
+  auto load_word = [&](uint32_t wi) -> uint32_t {
+    if (wi >= nwords) return 0u;
+    return a.r[(size_t)(wi >> 2) * cstride + (size_t)(qwave + lane_id()) * 4 + (wi & 3u)];
+  };
+  uint32_t pos = 0u, curw = 0u, nxtw = 0u;
+  bool need = false;
+  auto word_at = [&]() -> uint32_t { return curw >> (2u * (pos & 15u)); };
+  auto advance = [&]() {
+    ++pos;
+    if ((pos & 15u) == 0u) {
+      curw = nxtw;
+      need = true;
+    }
+  };
+  uint32_t R[2][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+  double lp = 0.0, lr = 0.0;
+  BsCursor cur;
+  cur.slot = -1; cur.pnx = -1; cur.hs = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u;
+  cur.cand = false; cur.plp = 0.0; cur.pc = 1u;
+  double plp2 = 0.0;
+  auto two_steps = [&]() -> bool { return a.t2 != nullptr && pos + 2u <= N; };
+  auto walk_prefetch = [&]() {
+    const uint32_t x = __builtin_amdgcn_alignbit(nxtw, curw, 2u * (pos & 15u));   // r of steps pos + 1, pos + 2
+    if (two_steps()) {
+      const uint32_t* e = a.t2 + ((size_t)cur.slot * 16u + (x & 15u)) * 8u;
+      const uint4 v = *reinterpret_cast<const uint4*>(e);
+      const uint2 w = *reinterpret_cast<const uint2*>(e + 4);
+      cur.pc = w.y;
+      cur.pnx = (int32_t)w.x;
+      plp2 = __hiloint2double((int)v.w, (int)v.z);
+      cur.plp = __hiloint2double((int)v.y, (int)v.x);
+    } else {
+      cur.prefetch_row(a, cur.slot, x & 3u);
+    }
+  };
+  uint32_t mode = kWalkDone;
+  int dec = 0;
+  auto finished = [&]() -> bool {
+    if (pos == N) return true;
+    if (a.early && (pos & (uint32_t)(kEarlyEvery - 1)) == 0u) dec = early_decide(lp, lr, (int64_t)(N - pos), a.lt_min, a.lp_min);
+    return dec != 0;
+  };
+  if (valid && N > 0u) {
+    curw = load_word(0u);
+    nxtw = load_word(1u);
+    cur.slot = a.slot0;   // D_0 = 0 is a learned row: every lane starts walking
+    walk_prefetch();
+    mode = kWalkWalk;
+  }
+  uint32_t phw = 0u;   // layout phase of the ACS lanes' planes (wave-uniform)
+  // one ACS step of the wave at phase PH (every lane computes; ACS lanes keep the result)
+  auto acs_step = [&](auto phc) {
+    constexpr int PH = decltype(phc)::value;
+    const uint32_t rr = word_at() & 3u;
+    uint32_t Nn[2][4], c;
+    bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
+    if (mode == kWalkAcs) {
+      cur.fence(Nn[1][3]);
+      cur.fence_keys(Nn[1][3]);
+      lp += cur.template resolve<PH>(a, R, rr, a.lp_unseen);   // Pd_plotter.py:115, T = P̂1
+      lr += s_lt[c];                                            // Pd_plotter.py:115, T = T_ref(1/2)
+      advance();
+      if (finished()) {
+        mode = kWalkDone;
+        cur.slot = -1;
+      } else {
+        cur.template prefetch<(PH + 1) % 6, false>(a, Nn, word_at() & 3u);   // hashed lookups
+        if (cur.slot >= 0) {
+          mode = kWalkWalk;
+          walk_prefetch();
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) R[r][i] = Nn[r][i];
+  };
+  const uint32_t wmin = (uint32_t)a.walk_wmin, amin = (uint32_t)a.walk_amin;
+  const int burst = a.walk_burst;
+  for (int64_t it = 0, it_max = 128 * ((int64_t)N + 1); it < it_max; ++it) {
+    if (need) {
+      nxtw = load_word((pos >> 4) + 1u);
+      need = false;
+    }
+    const uint64_t mA = __ballot(mode == kWalkAcs), mW = __ballot(mode == kWalkWalk);
+    if ((mA | mW) == 0u) break;
+    const uint32_t nA = (uint32_t)__popcll(mA), nW = (uint32_t)__popcll(mW);
+    if (nW != 0u && (nA == 0u || nW >= wmin || nA < amin)) {
+      for (int b = 0; b < burst; ++b) {
+        if (mode == kWalkWalk) {
+          // D_t is not a row: the lane joins the ACS steps with D_{t-1} = row `slot`, its
+          // planes the row's image at the wave's phase; that step takes log P̂1 from
+          // cur.plp with successor -1
+          auto leave = [&]() {
+            mode = kWalkAcs;
+            cur.pnx = -1;
+            const uint32_t* kp = a.dkey + (size_t)cur.slot * kBsDkeyWords + 8u * phw;
+            const uint4 u = *reinterpret_cast<const uint4*>(kp), v = *reinterpret_cast<const uint4*>(kp + 4);
+            R[0][0] = u.x; R[0][1] = u.y; R[0][2] = u.z; R[0][3] = u.w;
+            R[1][0] = v.x; R[1][1] = v.y; R[1][2] = v.z; R[1][3] = v.w;
+          };
+          auto done = [&]() {
+            mode = kWalkDone;
+            cur.slot = -1;
+          };
+          if (two_steps()) {
+            const int32_t d1 = (int32_t)((uint32_t)cur.pnx & 0x0FFFFFFFu) - 1;
+            if (d1 < 0) {
+              leave();
+            } else {
+              lp += cur.plp;                 // Pd_plotter.py:115, from the row's records
+              lr += s_lt[(uint32_t)cur.pnx >> 28];
+              cur.slot = d1;
+              advance();
+              if (finished()) {
+                done();
+              } else {
+                const int32_t d2 = (int32_t)(cur.pc & 0x0FFFFFFFu) - 1;
+                if (d2 < 0) {
+                  cur.plp = plp2;
+                  leave();
+                } else {
+                  lp += plp2;
+                  lr += s_lt[cur.pc >> 28];
+                  cur.slot = d2;
+                  advance();
+                  if (finished()) done();
+                  else walk_prefetch();
+                }
+              }
+            }
+          } else if (cur.pnx < 0) {
+            leave();
+          } else {
+            lp += cur.plp;                   // Pd_plotter.py:115, from the row's record
+            lr += s_lt[cur.pc];
+            cur.slot = cur.pnx;
+            advance();
+            if (finished()) done();
+            else walk_prefetch();
+          }
+        }
+        if (__ballot(mode == kWalkWalk) == 0u) break;
+      }
+      continue;
+    }
+    // two ACS steps of the wave (phases phw, phw + 1; phw is even); a lane the first sends
+    // back to a walk waits out the second
+    if (phw == 0u) {
+      acs_step(IntC<0>{});
+      acs_step(IntC<1>{});
+    } else if (phw == 2u) {
+      acs_step(IntC<2>{});
+      acs_step(IntC<3>{});
+    } else {
+      acs_step(IntC<4>{});
+      acs_step(IntC<5>{});
+    }
+    phw = phw == 4u ? 0u : phw + 2u;
+  }
+  // the guard is never reached (every iteration moves a lane); if it were, the partial
+  // sums must not pass for results (k1b_walk)
+  if (__ballot(mode != kWalkDone) != 0u && lane_id() == 0 && a.err) atomicOr(a.err, 1);
+  if (valid && a.sums) {
+    const int64_t qe = qwave + lane_id();
+    a.sums[2 * qe] = lp;
+    a.sums[2 * qe + 1] = lr;
+  }
+  early_final(dec, lp, lr);
+  count_decisions_masked(vmask, vmask, lp, lr, a.counts);
+}
+
+template <uint64_t XM>
+__device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
+  constexpr bool kUni = xm_uni<6, XM>();
+  __shared__ double s_lt[5];
+  if (threadIdx.x <= 4) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  fill_filter_patterns();
+  fill_bs_etab<XM>();
+#if CVD_K1B_LDSF
+  {   // the whole filter, 2 (fmask + 1) words, into dynamic LDS
+    uint4* d = reinterpret_cast<uint4*>(dyn_lds());
+    const uint4* g = reinterpret_cast<const uint4*>(a.filt);
+    for (uint32_t i = threadIdx.x; i < (a.fmask + 1u) / 2u; i += blockDim.x) d[i] = g[i];
+  }
+#endif
+  __syncthreads();
+  int64_t gw = (int64_t)blk * (kK1bBlock / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
+  if (a.walk) {
+    // H1 and H2 waves alternate on every SIMD (k1b_body)
+    const int64_t half = ((a.nseq + 63) / 64 + 1) / 2, k = gw >> 1;
+    if (gw < 2 * half) gw = ((gw ^ (gw >> 2)) & 1) ? half + k : k;
+  }
+  const int64_t qwave = gw * 64;
+  const int64_t q = qwave + lane_id();
+  const bool valid = q < a.nseq;
+  const uint64_t vmask = __ballot(valid), hmask = __ballot(q < a.n_h1);
+  if (a.walk && vmask != 0u && hmask == vmask) {
+    k1s_walk<XM>(a, qwave, vmask, s_lt);
+    return;
+  }
+  double lp = 0.0, lr = 0.0;
+  if (valid) {
+    uint32_t R[2][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};   // D_0 = 0
+    double lpu = a.lp_unseen;
+    asm volatile("" : "+v"(lpu));
+    const int64_t N = a.N, nwords = (N + 15) / 16;
+    const size_t cstride = (size_t)a.nseq * 4;
+    uint32_t c4[4];
+    auto load_chunk = [&](int64_t ci) {
+      const uint32_t* rb = a.r + (size_t)ci * cstride + (size_t)qwave * 4;
+      const uint4 v = 4 * ci < nwords ? *reinterpret_cast<const uint4*>(rb + lane_id() * 4u) : make_uint4(0u, 0u, 0u, 0u);
+      c4[0] = v.x; c4[1] = v.y; c4[2] = v.z; c4[3] = v.w;
+    };
+    auto pick = [&](int64_t wi) -> uint32_t {
+      const uint32_t e = (uint32_t)wi & 3u;
+      const uint32_t v = e == 0u ? c4[0] : e == 1u ? c4[1] : e == 2u ? c4[2] : c4[3];
+      return wi < nwords ? v : 0u;
+    };
+    // the received words as a 64-bit window (words wi, wi + 1) and the bit offset of the
+    // next step in it (< 32 at the top of a six-step group): one funnel shift per group,
+    // one bit-field extract per step
+    load_chunk(0);
+    uint32_t cw = pick(0), nw = pick(1);
+    int64_t wi = 0;
+    uint32_t sh = 0u;
+    BsCursor cur;
+    cur.start(a, cw & 3u);
+    auto step = [&](auto phc, uint32_t rr, uint32_t rn) {
+      constexpr int PH = decltype(phc)::value;
+      uint32_t Nn[2][4], c;
+      bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
+      cur.fence(Nn[1][3]);                       // Nn[1][3] depends on the whole ACS
+      cur.fence_keys(Nn[1][3]);
+      lp += cur.template resolve<PH>(a, R, rr, lpu);   // Pd_plotter.py:115, T = P̂1
+      lr += s_lt[c];                                   // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) R[r][i] = Nn[r][i];
+      cur.template prefetch<(PH + 1) % 6>(a, R, rn);
+    };
+    int64_t t = 0;
+    int grp = 0, dec = 0;
+    for (; t + 6 <= N; t += 6) {
+      const uint32_t win = __builtin_amdgcn_alignbit(nw, cw, sh);
+      step(IntC<0>{}, bits2(win, 0), bits2(win, 2));
+      step(IntC<1>{}, bits2(win, 2), bits2(win, 4));
+      step(IntC<2>{}, bits2(win, 4), bits2(win, 6));
+      step(IntC<3>{}, bits2(win, 6), bits2(win, 8));
+      step(IntC<4>{}, bits2(win, 8), bits2(win, 10));
+      step(IntC<5>{}, bits2(win, 10), bits2(win, 12));
+      sh += 12u;
+      if (sh >= 32u) {
+        sh -= 32u;
+        ++wi;
+        cw = nw;
+        nw = pick(wi + 1);
+        if (((wi + 1) & 3) == 3) load_chunk((wi + 2) >> 2);   // the word after nw opens a chunk
+      }
+      if (a.early && ++grp == kBsEarlyGroups) {
+        grp = 0;
+        if (!dec) dec = early_decide(lp, lr, N - (t + 6), a.lt_min, a.lp_min);
+        if (__ballot(dec == 0) == 0) {   // every lane decided: the wave is done
+          t = N;
+          break;
+        }
+      }
+    }
+    // last 1-5 steps
+    if (t < N) {
+      const uint32_t win = __builtin_amdgcn_alignbit(nw, cw, sh);
+      step(IntC<0>{}, bits2(win, 0), bits2(win, 2));
+      if (t + 1 < N) step(IntC<1>{}, bits2(win, 2), bits2(win, 4));
+      if (t + 2 < N) step(IntC<2>{}, bits2(win, 4), bits2(win, 6));
+      if (t + 3 < N) step(IntC<3>{}, bits2(win, 6), bits2(win, 8));
+      if (t + 4 < N) step(IntC<4>{}, bits2(win, 8), bits2(win, 10));
+    }
+    if (a.sums) {
+      const int64_t qe = qwave + lane_id();
+      a.sums[2 * qe] = lp;
+      a.sums[2 * qe + 1] = lr;
+    }
+    early_final(dec, lp, lr);
+  }
+  count_decisions_masked(vmask, hmask, lp, lr, a.counts);
+}
+
+template <uint64_t XM>
+__device__ __forceinline__ void k1s_multi(const MultiArgs& ma) {
+  const uint32_t b = blockIdx.x;
+  int i = 0;
+  uint32_t b0 = 0u;
+  while (i + 1 < ma.nm && b >= ma.blk_end[i]) b0 = ma.blk_end[i++];   // scalar: blockIdx is uniform
+  k1s_body<XM>(ma.a[i], b - b0);
+}
+
+// the specialised kernel's entries (cvd_rtc.cpp): the butterfly kernel, or for m = 6 its
+// bit-sliced form when the model's tables are the bit-sliced ones
+template <int m, uint64_t XM>
+__device__ __forceinline__ void k1b_spec_entry(const ExpArgs& a) {
+  if constexpr (CVD_K1B_BITSLICE && m == 6) k1s_body<XM>(a, blockIdx.x);
+  else k1b_body<m, true, XM, false>(a, blockIdx.x);
+}
+template <int m, uint64_t XM>
+__device__ __forceinline__ void k1b_spec_multi_entry(const MultiArgs& ma) {
+  if constexpr (CVD_K1B_BITSLICE && m == 6) k1s_multi<XM>(ma);
+  else k1b_multi<m, XM>(ma);
+}
+
+}  // namespace cvd_dev

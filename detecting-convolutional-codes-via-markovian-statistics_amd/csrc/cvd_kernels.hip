@@ -1665,7 +1665,8 @@ static int select_explicit(const cvd_model& M, int variant, ExpKernel* kern, con
 int cvd::explicit_kernel_of(const cvd_model& M) {
   ExpKernel k;
   const uint32_t* b;
-  return select_explicit(M, kExplicitBest, &k, &b);
+  const int which = select_explicit(M, kExplicitBest, &k, &b);
+  return which == CVD_KERNEL_BUTTERFLY_RTC && M.rtc_bs ? CVD_KERNEL_BITSLICE_RTC : which;
 }
 
 static int env_i(const char* name, int def) {
@@ -1708,22 +1709,27 @@ bool cvd::walk_preferred(const cvd_model& M, bool early) {
 static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int64_t N, int64_t nseq, int64_t n_h1,
                         double* d_sums, int64_t* d_counts, uint8_t* d_trace, const uint32_t* bmp, bool early) {
   ExpArgs a;
+  // the bit-sliced kernel (k1s) reads the bit-sliced tables, every other kernel the nibble ones
+  const bool bs = which == CVD_KERNEL_BUTTERFLY_RTC && M.rtc_bs;
   // (the LDS-filter kernel copies its own filter copy, the one with its smaller pattern table)
-  a.filt = which == CVD_KERNEL_BUTTERFLY_RTC && M.rtc_ldsf ? M.d_filt_lds : M.d_filt;
-  a.hkey = M.d_hkey; a.drow = M.d_drow; a.ltref = M.d_ltref;
+  a.filt = which == CVD_KERNEL_BUTTERFLY_RTC && M.rtc_ldsf ? (bs ? M.d_bfilt_lds : M.d_filt_lds)
+                                                            : (bs ? M.d_bfilt : M.d_filt);
+  a.hkey = bs ? M.d_bkey : M.d_hkey; a.drow = M.d_drow; a.ltref = M.d_ltref;
   // directory slots: keys [hcap][h_ssw dwords], records [hcap][h_rsw] or, interleaved
-  // (no separate record array), at dword nw of each key slot
-  a.hrow = M.d_hrow ? M.d_hrow : M.d_hkey + nib_words(M.dec.m);
-  a.ksh = (uint32_t)__builtin_ctz((unsigned)(4 * M.h_ssw));
-  a.rsh = M.d_hrow ? (uint32_t)__builtin_ctz((unsigned)(4 * M.h_rsw)) : a.ksh;
+  // (no separate record array), at dword nw of each key slot; bit-sliced: 64-dword slots
+  // whose layout the kernel knows (cvd_k1s.h)
+  a.hrow = bs ? M.d_bkey : M.d_hrow ? M.d_hrow : M.d_hkey + nib_words(M.dec.m);
+  a.ksh = bs ? 8u : (uint32_t)__builtin_ctz((unsigned)(4 * M.h_ssw));
+  a.rsh = bs ? 8u : M.d_hrow ? (uint32_t)__builtin_ctz((unsigned)(4 * M.h_rsw)) : a.ksh;
   a.bmp = bmp; a.slot0 = M.slot0;
   a.repmap = M.repmap; a.swmap = M.swmap; a.bfly_uni = M.bfly_uni;
   for (int w = 0; w < 4; ++w) a.bfly_even[w] = M.bfly_even[w];
-  a.hmask = (uint32_t)(M.hcap - 1); a.fmask = (uint32_t)(M.fcap / 2 - 1); a.fmask4 = a.fmask << 3; a.max_probe = M.max_probe; a.lp_unseen = M.logp1_unseen;
+  a.hmask = (uint32_t)((bs ? M.bhcap : M.hcap) - 1); a.fmask = (uint32_t)(M.fcap / 2 - 1); a.fmask4 = a.fmask << 3;
+  a.max_probe = bs ? M.bmax_probe : M.max_probe; a.lp_unseen = M.logp1_unseen;
   a.N = N; a.nseq = nseq; a.n_h1 = n_h1; a.r = d_r; a.sums = d_sums; a.counts = d_counts;
   a.trace = d_trace;
   a.early = early && !d_sums && !d_trace; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
-  a.dkey = M.d_dkey;
+  a.dkey = bs ? M.d_bdkey : M.d_dkey;
   a.err = M.d_err;
   a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
@@ -1820,6 +1826,10 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_drow, M.h_drow))) return rc;
     if ((rc = dev_copy(M.d_dkey, M.h_dkey))) return rc;
     if ((rc = dev_copy(M.d_t2, M.h_t2))) return rc;
+    if ((rc = dev_copy(M.d_bfilt, M.h_bfilt))) return rc;
+    if ((rc = dev_copy(M.d_bfilt_lds, M.h_bfilt_lds))) return rc;
+    if ((rc = dev_copy(M.d_bkey, M.h_bkey))) return rc;
+    if ((rc = dev_copy(M.d_bdkey, M.h_bdkey))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
     if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
     if ((rc = dev_copy(M.d_bfly, M.bfly))) return rc;
@@ -1842,15 +1852,26 @@ int cvd::upload_model(cvd_model& M, int device) {
   // else 256 (CVD_K1B_BLOCK=256/512/1024 overrides, timing studies)
   M.rtc_block = env_i("CVD_K1B_BLOCK", M.rtc_ldsf ? 512 : kBlock);
   if (M.rtc_block != 256 && M.rtc_block != 512 && M.rtc_block != 1024) M.rtc_block = kBlock;
-  const std::string vdefs = "-DCVD_K1B_BLOCK=" + std::to_string(M.rtc_block) +
-                            (M.rtc_ldsf ? " -DCVD_K1B_LDSF=1 -DCVD_FILTER_PAT_BITS=" + std::to_string(kFilterPatBitsLds) : "");
-  if (M.k1b_ok && M.hcap > 0 &&
-      rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn, &M.rtc_fn_multi) != 0) {
+  // the bit-sliced form (k1s) for models with the bit-sliced tables; if it cannot be
+  // built, the butterfly kernel on the nibble tables
+  M.rtc_bs = false;
+  for (int attempt = M.bs && M.d_bkey ? 0 : 1; attempt < 2 && M.k1b_ok && M.hcap > 0; ++attempt) {
+    const bool bs = attempt == 0;
+    const std::string vdefs = "-DCVD_K1B_BLOCK=" + std::to_string(M.rtc_block) +
+                              (M.rtc_ldsf ? " -DCVD_K1B_LDSF=1 -DCVD_FILTER_PAT_BITS=" + std::to_string(kFilterPatBitsLds) : "") +
+                              (bs ? " -DCVD_K1B_BITSLICE=1" : "");
+    if (rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn, &M.rtc_fn_multi) == 0) {
+      M.rtc_bs = bs;
+      M.jit_error.clear();
+      break;
+    }
     M.rtc_fn = nullptr;
     M.rtc_fn_multi = nullptr;
+    M.jit_error = last_error_copy();
+  }
+  if (!M.rtc_fn) {
     M.rtc_ldsf = false;
     M.rtc_block = kBlock;
-    M.jit_error = last_error_copy();
   }
   return CVD_OK;
 }
@@ -1861,11 +1882,13 @@ void cvd::free_model_device(cvd_model& M) {
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
   void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_filt_lds, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
-                  M.d_bmk1, M.d_bfly, M.d_err};
+                  M.d_bmk1, M.d_bfly, M.d_err, M.d_bfilt, M.d_bfilt_lds, M.d_bkey, M.d_bdkey};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
   M.d_filt = nullptr; M.d_filt_lds = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_t2 = nullptr;
+  M.d_bfilt = nullptr; M.d_bfilt_lds = nullptr; M.d_bkey = nullptr; M.d_bdkey = nullptr;
+  M.rtc_bs = false;
   M.d_bmp = nullptr;
   M.d_bmk1 = nullptr;
   M.d_bfly = nullptr;
@@ -1951,7 +1974,17 @@ static bool multi_ok(const cvd_model& M) {
 }
 static bool multi_same(const cvd_model& A, const cvd_model& B) {
   return A.rtc_fn_multi == B.rtc_fn_multi && A.rtc_block == B.rtc_block && A.rtc_ldsf == B.rtc_ldsf &&
-         A.device == B.device && (!A.rtc_ldsf || A.fcap == B.fcap);
+         A.rtc_bs == B.rtc_bs && A.device == B.device && (!A.rtc_ldsf || A.fcap == B.fcap);
+}
+// the same criterion as one id (cvd_model_info.multi_variant: the Python host groups launches
+// for per-launch timing by it): equal for models multi_same merges, 0 if multi_ok fails
+int64_t cvd::multi_variant(const cvd_model& M) {
+  if (!multi_ok(M)) return 0;
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+  mix((uint64_t)(uintptr_t)M.rtc_fn_multi); mix((uint64_t)M.rtc_block); mix(M.rtc_ldsf ? 1u : 0u);
+  mix(M.rtc_bs ? 1u : 0u); mix((uint64_t)(M.device + 1)); mix(M.rtc_ldsf ? (uint64_t)M.fcap : 0u);
+  return (int64_t)(h | 1u);
 }
 
 extern "C" int cvd_detect_multi(const cvd_model* const* models, int32_t nm, const uint32_t* const* d_r, int64_t N,

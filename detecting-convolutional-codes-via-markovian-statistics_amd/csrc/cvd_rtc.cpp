@@ -94,14 +94,15 @@ const char* kClangFlags[] = {"-O3", "-std=c++17", "-ffp-contract=off",
                              // interleaved A/B (profiles/r01g_ab/), same registers, no spills
                              "-mllvm", "--amdgpu-sched-strategy=max-ilp"};
 
-// two entries per code: one model per launch, and several (k1b_multi, cvd_detect_multi)
+// two entries per code: one model per launch, and several (k1b_multi, cvd_detect_multi);
+// the model's variant defines pick the butterfly kernel or its bit-sliced form (k1s)
 std::string entry_source(int m, uint64_t xm) {
   char entry[640];
   std::snprintf(entry, sizeof(entry),
                 "\nextern \"C\" __global__ __launch_bounds__(cvd_dev::kK1bBlock, cvd_dev::kK1bWavesPerSimd)\n"
-                "void cvd_k1b_spec(cvd_dev::ExpArgs a) { cvd_dev::k1b_body<%d, true, 0x%016llxull, false>(a, blockIdx.x); }\n"
+                "void cvd_k1b_spec(cvd_dev::ExpArgs a) { cvd_dev::k1b_spec_entry<%d, 0x%016llxull>(a); }\n"
                 "extern \"C\" __global__ __launch_bounds__(cvd_dev::kK1bBlock, cvd_dev::kK1bWavesPerSimd)\n"
-                "void cvd_k1b_spec_multi(cvd_dev::MultiArgs a) { cvd_dev::k1b_multi<%d, 0x%016llxull>(a); }\n",
+                "void cvd_k1b_spec_multi(cvd_dev::MultiArgs a) { cvd_dev::k1b_spec_multi_entry<%d, 0x%016llxull>(a); }\n",
                 m, (unsigned long long)xm, m, (unsigned long long)xm);
   return entry;
 }

@@ -5,6 +5,9 @@ butterfly kernel for one decoder, compiled here exactly as cvd_rtc.cpp does it
 
   python3 spec_resource.py [m6|m2|...] [-DCVD_K1B_WAVES=5 ...] [--isa out.s]
 
+(-DCVD_K1B_BITSLICE=1: the bit-sliced m = 6 form, k1s, as cvd_rtc.cpp builds it for models
+with bit-sliced tables)
+
 No GPU needed: the code constant (out(j, 0) of every butterfly) comes from the
 host tables (cvd_code_tables), as build_bfly computes it.
 """
@@ -41,9 +44,9 @@ def main():
         with open(src, "w") as f:
             f.write('#include <hip/hip_runtime.h>\n#include "cvd_device.h"\n'
                     'extern "C" __global__ __launch_bounds__(cvd_dev::kBlock, cvd_dev::kK1bWavesPerSimd)\n'
-                    f'void cvd_k1b_spec(cvd_dev::ExpArgs a) {{ cvd_dev::k1b_body<{m}, true, 0x{xm:016x}ull, false>(a, blockIdx.x); }}\n'
+                    f'void cvd_k1b_spec(cvd_dev::ExpArgs a) {{ cvd_dev::k1b_spec_entry<{m}, 0x{xm:016x}ull>(a); }}\n'
                     'extern "C" __global__ __launch_bounds__(cvd_dev::kBlock, cvd_dev::kK1bWavesPerSimd)\n'
-                    f'void cvd_k1b_spec_multi(cvd_dev::MultiArgs a) {{ cvd_dev::k1b_multi<{m}, 0x{xm:016x}ull>(a); }}\n')
+                    f'void cvd_k1b_spec_multi(cvd_dev::MultiArgs a) {{ cvd_dev::k1b_spec_multi_entry<{m}, 0x{xm:016x}ull>(a); }}\n')
         base = [clang, "-x", "hip", "--offload-arch=gfx950", "--offload-device-only", "--no-gpu-bundle-output",
                 "-O3", "-std=c++17", "-ffp-contract=off", "-mllvm", "--amdgpu-sched-strategy=max-ilp",
                 "-I", HERE, *defs]

@@ -329,11 +329,11 @@ class Detector:
     @staticmethod
     def multi_groups(models):
         """Index runs of `models` that cvd_detect_multi merges into one launch (the same
-        specialised kernel variant; at most 8 per launch) -- for per-launch timing."""
+        specialised kernel variant, as the library reports it: cvd_model_info.multi_variant;
+        at most 8 per launch) -- for per-launch timing."""
         groups, cur, key = [], [], None
         for i, m in enumerate(models):
-            inf = m.info()
-            k = (inf["explicit_kernel"], inf["lds_filter"]) if inf["kind"] == 1 and inf["explicit_kernel"] == 4 else None
+            k = m.info()["multi_variant"] or None
             if cur and (k is None or k != key or len(cur) == 8 or os.environ.get("CVD_NO_MULTI")):
                 groups.append(cur)
                 cur = []

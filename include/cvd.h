@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 8
+#define CVD_ABI_VERSION 9
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -93,6 +93,10 @@ typedef struct cvd_model_info {
   int32_t lds_filter;      /* 1: the specialised kernel keeps this model's Bloom filter in LDS (walking
                               models of <= 32,768 rows, filter built with 64 KiB, 512-thread blocks;
                               CVD_NO_LDSF=1 keeps it in global memory) */
+  int32_t pad0;
+  int64_t multi_variant;   /* nonzero: the specialised kernel variant this model runs in a
+                              cvd_detect_multi launch; consecutive models with equal nonzero values
+                              share one launch (at most 8).  0: the model is detected on its own */
 } cvd_model_info;
 
 #define CVD_KERNEL_NONE 0       /* explicit path unsupported for this shape */
@@ -100,6 +104,8 @@ typedef struct cvd_model_info {
 #define CVD_KERNEL_ORBIT 2      /* detect_k1_kernel<m,n>: k = 1, ACS for the 2^n/2 orbit representatives */
 #define CVD_KERNEL_BUTTERFLY 3  /* detect_k1b_kernel<m>: k = 1, n = 2 standard butterflies, one ACS vector */
 #define CVD_KERNEL_BUTTERFLY_RTC 4  /* the same, specialised to the decoder code at model upload (JIT, cvd_rtc.cpp) */
+#define CVD_KERNEL_BITSLICE_RTC 5   /* m = 6: its bit-sliced form (k1s, cvd_k1s.h: four bit-planes of two words
+                                       per lane, the row tables keyed by a canonical digest; same sums) */
 
 typedef struct cvd_model cvd_model;
 

@@ -24,7 +24,10 @@ by exec-mask branches: filter-positive loads, key compare, probing, hashing), wi
 their static VALU counts.  A wave executes a conditional block whenever ANY of its
 64 lanes takes it, so for the mixed lanes of a wave most of them run every step.
 
-  python profiles/isa_breakdown.py [m6] [--isa out.s] [-D...]
+  python profiles/isa_breakdown.py [m6] [--isa out.s] [-D...] [--steps S --nth K]
+
+(-DCVD_K1B_BITSLICE=1: the bit-sliced kernel k1s, six steps per iteration; its classes are
+the opcode classes above, which for k1s mostly land in "logic" (v_bitop3) and "pack" (v_perm))
 """
 import collections
 import json
@@ -44,16 +47,24 @@ def build_isa(cfg, defs, path):
     return open(path).read().splitlines()
 
 
-def main_loop(lines):
+def main_loop(lines, nth=0):
     """Lines of the largest outermost loop (Depth=1) of the kernel body (the step
-    loop; the prologue's LDS table fill is a small loop of its own)."""
-    best = None
-    for hdr in (i for i, l in enumerate(lines) if "Loop Header: Depth=1" in l):
+    loop; the prologue's LDS table fill is a small loop of its own).  nth = 1: the loop with
+    the most v_bitop3 (the bit-sliced kernel's lockstep loop)."""
+    found = []
+    end = next((i for i, l in enumerate(lines) if l.startswith(".Lfunc_end")), len(lines))
+    for hdr in (i for i, l in enumerate(lines[:end]) if "Loop Header: Depth=1" in l):
         label = lines[hdr].split(":")[0]
-        backs = [i for i, l in enumerate(lines) if re.search(r"\bs_(c)?branch\w*\s+" + re.escape(label) + r"\b", l)]
-        if backs and (best is None or max(backs) - hdr > best[1] - best[0]):
-            best = (hdr, max(backs))
-    return lines[best[0]:best[1] + 1]
+        backs = [i for i, l in enumerate(lines[:end]) if re.search(r"\bs_(c)?branch\w*\s+" + re.escape(label) + r"\b", l)]
+        if backs:
+            size = max(backs) - hdr
+            if nth == 1:   # k1s: the lockstep loop is the one with the most bit-sliced logic
+                size = sum("v_bitop3" in l for l in lines[hdr:max(backs) + 1])
+            found.append((size, hdr, max(backs)))
+    found.sort(reverse=True)
+    nth = 0
+    _, a, b = found[nth]
+    return lines[a:b + 1]
 
 
 def blocks(loop):
@@ -116,13 +127,24 @@ def main():
         i = args.index("--isa")
         isa = args[i + 1]
         del args[i:i + 2]
+    steps, nth = 4, 0
+    if "--steps" in args:
+        i = args.index("--steps")
+        steps = int(args[i + 1])
+        del args[i:i + 2]
+    if "--nth" in args:
+        i = args.index("--nth")
+        nth = int(args[i + 1])
+        del args[i:i + 2]
+    if "-DCVD_K1B_BITSLICE=1" in args and steps == 4:
+        steps, nth = 6, 1     # k1s: six steps per lockstep iteration
     defs = [a for a in args if a.startswith("-")]
     rest = [a for a in args if not a.startswith("-")]
     cfg = rest[0] if rest else "m6"
     with tempfile.TemporaryDirectory() as d:
         path = isa or os.path.join(d, "k.s")
         lines = build_isa(cfg, defs, path)
-    loop = main_loop(lines)
+    loop = main_loop(lines, nth)
     bl = blocks(loop)
     # straight-line blocks: not entered through an exec-mask branch (s_and_saveexec /
     # s_cbranch_execz in the preceding block) and not part of the probe loops
@@ -144,7 +166,6 @@ def main():
         guarded = any(x.startswith("s_cbranch_execz") for x in ins[-2:])
         if any(x.startswith("s_or_b64 exec") for x in ins[:2]):
             guarded = False
-    steps = 4
     out = {
         "kernel": "cvd_k1b_spec", "config": cfg, "defines": defs, "steps_per_iteration": steps,
         "valu_per_step_always": {k: v / steps for k, v in sorted(always.items())},

@@ -1,0 +1,179 @@
+// Host check of the bit-sliced m = 6 step (csrc/cvd_bitslice.h) against the plain Eq. 4-5
+// recursion (viterbi_markov.py:139-159), compiled with g++ by tests/test_bitslice_host.py.
+// For each received word of a few streams (random words; G1- and G2-encoded words through
+// a BSC) and every layout phase it checks: the new planes equal the phase-(f+1) image of
+// the reference step's D_t; mu equals the step's minimum; c equals the number of words
+// r' with step(D, r') == D_t (the T_ref count, Pd_plotter.py:89-99); the digest hash of
+// the new planes equals the host key of D_t (bs_digest + key_hash), and bs_canon<f> maps
+// every phase-f digest image to the phase-0 one.  TEST INFRASTRUCTURE ONLY.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cstdint>
+
+#include "../detecting-convolutional-codes-via-markovian-statistics_amd/csrc/cvd_bitslice.h"
+
+using namespace cvd;
+
+static int parity(unsigned x) { return __builtin_popcount(x) & 1; }
+
+struct Code {
+  unsigned g[2];   // bit 0 = input tap, bit d = state bit d - 1 (cvd_common.h enc_out)
+  unsigned out(unsigned s, unsigned u) const {
+    unsigned o = 0;
+    for (int j = 0; j < 2; ++j) o |= (unsigned)parity(g[j] & (u | (s << 1))) << j;
+    return o;
+  }
+};
+
+static Code code_of(const char* a, const char* b) {
+  Code c;
+  const char* t[2] = {a, b};
+  for (int j = 0; j < 2; ++j) {
+    c.g[j] = 0;
+    for (int d = 0; t[j][d]; ++d) c.g[j] |= (unsigned)(t[j][d] - '0') << d;
+  }
+  return c;
+}
+
+static unsigned g_rng = 12345u;
+static unsigned rnd() {
+  g_rng = g_rng * 1664525u + 1013904223u;
+  return g_rng >> 8;
+}
+
+// reference step: D' before normalisation, and normalised
+static void ref_step(const Code& dec, const uint8_t* D, unsigned y, uint8_t* out, int* mn_out) {
+  int best[64];
+  for (int x = 0; x < 64; ++x) best[x] = 1000;
+  for (int s = 0; s < 64; ++s)
+    for (unsigned u = 0; u < 2; ++u) {
+      const int v = D[s] + __builtin_popcount(dec.out((unsigned)s, u) ^ y);
+      const int ns = (int)((u | ((unsigned)s << 1)) & 63u);
+      if (v < best[ns]) best[ns] = v;
+    }
+  int mn = 1000;
+  for (int x = 0; x < 64; ++x) mn = best[x] < mn ? best[x] : mn;
+  for (int x = 0; x < 64; ++x) out[x] = (uint8_t)(best[x] - mn);
+  *mn_out = mn;
+}
+
+template <int PH, bool kUni>
+static void run_step(const bs_u32 (&R)[2][4], const BsE& E, bs_u32 (&N)[2][4], bs_u32& mu, bs_u32& c, bs_u32& hph,
+                     bs_u32& hpl) {
+  bs_step_core<PH, kUni>(R, E.e0, E.e1, E.ez, N, mu, c);
+  bs_digest_hash<(PH + 1) % 6>(N, hph, hpl);
+}
+
+template <bool kUni>
+static void step_any(int ph, const bs_u32 (&R)[2][4], const BsE& E, bs_u32 (&N)[2][4], bs_u32& mu, bs_u32& c,
+                     bs_u32& hph, bs_u32& hpl) {
+  switch (ph) {
+    case 0: run_step<0, kUni>(R, E, N, mu, c, hph, hpl); break;
+    case 1: run_step<1, kUni>(R, E, N, mu, c, hph, hpl); break;
+    case 2: run_step<2, kUni>(R, E, N, mu, c, hph, hpl); break;
+    case 3: run_step<3, kUni>(R, E, N, mu, c, hph, hpl); break;
+    case 4: run_step<4, kUni>(R, E, N, mu, c, hph, hpl); break;
+    default: run_step<5, kUni>(R, E, N, mu, c, hph, hpl); break;
+  }
+}
+
+static void canon_any(int ph, bs_u32& lo, bs_u32& hi) {
+  switch (ph) {
+    case 0: bs_canon<0>(lo, hi); break;
+    case 1: bs_canon<1>(lo, hi); break;
+    case 2: bs_canon<2>(lo, hi); break;
+    case 3: bs_canon<3>(lo, hi); break;
+    case 4: bs_canon<4>(lo, hi); break;
+    default: bs_canon<5>(lo, hi); break;
+  }
+}
+
+static int fail(const char* what, long t, int ph) {
+  std::printf("FAIL %s at step %ld phase %d\n", what, t, ph);
+  return 1;
+}
+
+int main(int argc, char** argv) {
+  const long steps = argc > 1 ? std::atol(argv[1]) : 20000;
+  const Code dec = code_of("1011011", "1111001"), enc2 = code_of("1111001", "1011011");   // (133,171) / (171,133)
+  // butterfly symmetry the layout relies on (build_bfly)
+  bs_u64 xm = 0;
+  bool uni = true;
+  for (unsigned j = 0; j < 32; ++j) {
+    const unsigned x = dec.out(j, 0);
+    if (dec.out(j, 1) != (x ^ 3u) || dec.out(j + 32, 0) != (x ^ 3u) || dec.out(j + 32, 1) != x) {
+      std::printf("FAIL not a standard butterfly code\n");
+      return 1;
+    }
+    xm |= (bs_u64)x << (2 * j);
+    if (parity(x)) uni = false;
+  }
+  long checked = 0, c_counts[5] = {0, 0, 0, 0, 0}, mu1 = 0;
+  int dmax = 0;
+  // streams: 0 uniform random words, 1 G1-encoded + BSC(0.05), 2 G2-encoded + BSC(0.05), 3 G1 + BSC(0.2)
+  for (int stream = 0; stream < 4; ++stream) {
+    uint8_t D[64], Dn[64];
+    std::memset(D, 0, sizeof(D));
+    unsigned es = 0;
+    const Code& enc = stream == 2 ? enc2 : dec;
+    const unsigned thr = stream == 3 ? 200u : 50u;
+    for (long t = 0; t < steps; ++t) {
+      const int ph = (int)(t % 6);
+      unsigned y;
+      if (stream == 0) {
+        y = rnd() & 3u;
+      } else {
+        const unsigned u = rnd() & 1u;
+        y = enc.out(es, u);
+        es = (u | (es << 1)) & 63u;
+        for (int b = 0; b < 2; ++b)
+          if (rnd() % 1000u < thr) y ^= 1u << b;
+      }
+      bs_u32 img[8];
+      bs_image(D, ph, img);
+      // digest canonicalisation of this phase's image
+      {
+        bs_u32 lo = img[0] ^ img[1], hi = img[4] ^ img[5], z[2];
+        canon_any(ph, lo, hi);
+        bs_digest(D, z);
+        if (lo != z[0] || hi != z[1]) return fail("bs_canon", t, ph);
+      }
+      bs_u32 R[2][4], N[2][4];
+      for (int r = 0; r < 2; ++r)
+        for (int i = 0; i < 4; ++i) R[r][i] = img[4 * r + i];
+      const BsE E = bs_eplanes(xm, ph, y);
+      bs_u32 mu, c, hph, hpl;
+      if (uni) step_any<true>(ph, R, E, N, mu, c, hph, hpl);
+      else step_any<false>(ph, R, E, N, mu, c, hph, hpl);
+      int mn;
+      ref_step(dec, D, y, Dn, &mn);
+      bs_u32 want[8];
+      bs_image(Dn, (ph + 1) % 6, want);
+      for (int r = 0; r < 2; ++r)
+        for (int i = 0; i < 4; ++i)
+          if (N[r][i] != want[4 * r + i]) return fail("planes", t, ph);
+      if ((int)mu != mn) return fail("mu", t, ph);
+      unsigned cref = 0;
+      for (unsigned q = 0; q < 4; ++q) {
+        uint8_t Dq[64];
+        int mq;
+        ref_step(dec, D, q, Dq, &mq);
+        cref += std::memcmp(Dq, Dn, 64) == 0;
+      }
+      if (c != cref) return fail("T_ref count", t, ph);
+      bs_u32 z[2], kph, kpl;
+      bs_digest(Dn, z);
+      key_hash(z, 2, kph, kpl);
+      if (kph != hph || kpl != hpl) return fail("digest hash", t, ph);
+      for (int s = 0; s < 64; ++s) dmax = Dn[s] > dmax ? Dn[s] : dmax;
+      c_counts[c]++;
+      mu1 += mu;
+      std::memcpy(D, Dn, 64);
+      ++checked;
+    }
+  }
+  std::printf("ok steps=%ld uni=%d max_D=%d mu1=%ld c1=%ld c2=%ld c3=%ld c4=%ld\n", checked, (int)uni, dmax, mu1,
+              c_counts[1], c_counts[2], c_counts[3], c_counts[4]);
+  return 0;
+}

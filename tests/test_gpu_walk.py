@@ -152,7 +152,8 @@ def test_lds_filter_model_under_jit_fallbacks(pkg, monkeypatch, how):
     inf = alt.info()
     # info.walk reports what runs: walk mode needs the specialised kernel
     if how == "hiprtc":
-        assert inf["explicit_kernel"] == 4 and inf["lds_filter"] == 1 and inf["walk"] == 1
+        # (the bit-sliced form k1s if the hipRTC compiler takes it, else the butterfly kernel)
+        assert inf["explicit_kernel"] in (4, 5) and inf["lds_filter"] == 1 and inf["walk"] == 1
     else:
         assert inf["explicit_kernel"] == 3 and inf["lds_filter"] == 0 and inf["walk"] == 0
     got, gc = _sums(det, alt, cc, N, p, t0, t1)
