@@ -379,6 +379,7 @@ def main():
     ev = make_events(a.steps)
     t0 = time.perf_counter()
     run(a.steps, 0, ev)
+    shard = counts.clone() if dist else None   # this rank's own counts (reduce_record checks the reduce)
     if dist:
         dist.all_reduce(counts)                # the one collective: success counts over RCCL
     torch.cuda.synchronize()
@@ -452,6 +453,8 @@ def main():
                              "headline value above runs every step of every trial"}
         counts.copy_(full_counts)
 
+    dist_rec = reduce_record(dist, shard, counts, world, rank,
+                             f"rank r takes global trial ids [(s W + r) B, (s W + r + 1) B) of step s, B = {B}")
     # per-rank setup (model learning on the GPU + the JIT compile of the specialised kernel,
     # every rank at once): the multi-rank rehearsal's evidence, one entry per rank
     setup_by_rank = [{"rank": rank, "setup_s": t_setup, "host": socket.gethostname(), "device": local}]
@@ -575,6 +578,7 @@ def main():
                    "model": info["kind"] and "sparse(learned)" or "dense",
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
+        "distributed": dist_rec,
         "roofline": {"bound": "lds" if lds_diag else "valu" if valu else "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -686,6 +690,7 @@ def run_c4(a, pkg, world, rank, local, dist):
         per_n_s.append(time.perf_counter() - tn)
         print(json.dumps({"c4_progress": {"rank": rank, "N": N, "seconds": per_n_s[-1]}}), file=sys.stderr,
               flush=True)
+    shard = counts.clone() if dist else None
     if dist:
         dist.all_reduce(counts)                  # the one collective: success counts over RCCL
     torch.cuda.synchronize()
@@ -693,6 +698,8 @@ def run_c4(a, pkg, world, rank, local, dist):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    dist_rec = reduce_record(dist, shard, counts, world, rank,
+                             f"rank r takes global trial ids [r T / W, (r + 1) T / W) of every grid point, T = {T}")
     if dist:
         dev = det.device if a.dist_backend == "nccl" else "cpu"
         t = torch.tensor([elapsed] + per_n_s, device=dev, dtype=torch.float64)
@@ -750,6 +757,7 @@ def run_c4(a, pkg, world, rank, local, dist):
                      "basis": "algorithmic stream bytes of every grid point (SURVEY §8(d)) over the whole timed "
                               "region (generator + detector); per N in per_N[N].roofline"},
         "counts": c.tolist(),
+        "distributed": dist_rec,
         "diagnostic": {"model_setup_s": t_setup, "elapsed_s": elapsed},
     }
     if a.cpu_baseline and world == 1:
@@ -758,6 +766,32 @@ def run_c4(a, pkg, world, rank, local, dist):
     print(json.dumps(out, default=_json_default), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def reduce_record(dist, shard, reduced, world, rank, sharding):
+    """The multi-GPU run checks itself: the communicator holds `world` ranks, and the
+    reduced success counts equal the sum of every rank's own counts (gathered to the host
+    after the timed region).  A wrong-rank, partial or double reduce raises instead of
+    printing a line; the record (communicator size, backend, each rank's shard) goes into
+    the bench line."""
+    import numpy as np
+    if not dist:
+        return {"backend": None, "world_size": 1, "shards_sum_equals_reduced": True, "sharding": sharding}
+    size = dist.get_world_size()
+    mine = {"rank": rank, "counts": shard.cpu().tolist()}
+    lst = [None] * size
+    dist.all_gather_object(lst, mine)
+    total = None
+    for e in lst:
+        v = np.asarray(e["counts"], dtype=np.int64)
+        total = v if total is None else total + v
+    red = reduced.cpu().numpy()
+    ok = size == world and sorted(e["rank"] for e in lst) == list(range(world)) and np.array_equal(total, red)
+    if not ok:
+        raise RuntimeError(f"count reduce check failed: communicator size {size} (expected {world}), ranks "
+                           f"{sorted(e['rank'] for e in lst)}, sum of shards {total.tolist()} != reduced {red.tolist()}")
+    return {"backend": str(dist.get_backend()), "world_size": size, "shards_sum_equals_reduced": True,
+            "rank_shards": [e["counts"] for e in sorted(lst, key=lambda e: e["rank"])], "sharding": sharding}
 
 
 def _json_default(o):

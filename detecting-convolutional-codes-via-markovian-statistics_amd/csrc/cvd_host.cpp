@@ -514,8 +514,8 @@ void build_hash(cvd_model& Mo) {
   // so that the specialised kernel keeps the whole filter in LDS (ldsf_preferred,
   // cvd_kernels.hip): up to 4 keys per two-word block, ~0.06% false positives, against an
   // L2 read per H2 step.
-  const bool ldsf = walk_preferred(Mo) && Mo.n_rows <= kLdsFilterMaxRows && !std::getenv("CVD_NO_LDSF");
-  int fscale = 0, fmax_log2 = ldsf ? kLdsFilterLog2 : 19;
+  const bool ldsf = walk_preferred(Mo) && Mo.n_rows <= ldsf_max_rows() && !std::getenv("CVD_NO_LDSF");
+  int fscale = 0, fmax_log2 = ldsf ? ldsf_log2() : 19;
   if (const char* e = std::getenv("CVD_FILTER_SCALE")) fscale = std::max(-3, std::min(3, std::atoi(e)));
   if (const char* e = std::getenv("CVD_FILTER_MAX_LOG2")) fmax_log2 = std::max(8, std::min(28, std::atoi(e)));
   while ((fscale >= 0 ? fcap >> fscale : fcap << -fscale) < Mo.n_rows && fcap < ((int64_t)1 << fmax_log2)) fcap <<= 1;
@@ -612,6 +612,10 @@ void build_hash(cvd_model& Mo) {
   if (Mo.bs) {
     int bload = 3;
     if (const char* e = std::getenv("CVD_BS_LOAD_LOG2")) bload = std::max(1, std::min(5, std::atoi(e)));
+    // the filter's pattern table (kernel LDS: 8 B per pattern pair); CVD_BS_PAT_BITS 8..12
+    Mo.bs_pat_bits = kFilterPatBits;
+    if (const char* e = std::getenv("CVD_BS_PAT_BITS")) Mo.bs_pat_bits = std::max(8, std::min(kFilterPatBits, std::atoi(e)));
+    const unsigned bnpat = 1u << Mo.bs_pat_bits;
     int64_t bcap = 64;
     while (bcap < ((int64_t)1 << bload) * Mo.n_rows) bcap <<= 1;
     Mo.bhcap = bcap;
@@ -631,8 +635,8 @@ void build_hash(cvd_model& Mo) {
     for (int64_t i = 0; i < Mo.n_rows; ++i) {
       const uint32_t ph = bph[(size_t)i], pl = bpl[(size_t)i];
       const size_t fb = (size_t)filter_block_index(pl, (uint32_t)(fcap / 2 - 1));
-      Mo.h_bfilt[2 * fb] |= filter_pattern(filter_pattern_index(ph, npat));
-      Mo.h_bfilt[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph, npat), npat);
+      Mo.h_bfilt[2 * fb] |= filter_pattern(filter_pattern_index(ph, bnpat));
+      Mo.h_bfilt[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph, bnpat), bnpat);
       if (ldsf) {
         const unsigned nl = 1u << kFilterPatBitsLds;
         Mo.h_bfilt_lds[2 * fb] |= filter_pattern(filter_pattern_index(ph, nl));
@@ -659,7 +663,10 @@ void build_hash(cvd_model& Mo) {
   // (r1, r2), 32 B {log P̂1(d, r1), log P̂1(d1, r2), (d1 + 1) | c(d, r1) << 28,
   // (d2 + 1) | c(d1, r2) << 28}, d1 / d2 the rows after one / two steps (0 = not a row)
   Mo.h_t2.clear();
-  if (Mo.dec.k == 1 && R == 4 && walk_preferred(Mo)) {
+  // (the bit-sliced kernel's lockstep lanes read them too: a lane walking learned rows loads
+  // one record per two steps; CVD_BS_T2=0 leaves them to the walking models)
+  const char* bt2 = std::getenv("CVD_BS_T2");
+  if (Mo.dec.k == 1 && R == 4 && (walk_preferred(Mo) || (Mo.bs && !(bt2 && bt2[0] == '0')))) {
     Mo.h_t2.assign((size_t)Mo.n_rows * 16 * 8, 0u);
     parallel_for(Mo.n_rows, [&](int64_t d, int) {
       const uint32_t* a0 = Mo.h_drow.data() + (size_t)d * Mo.h_rsw;
@@ -758,6 +765,15 @@ void build_bmp(cvd_model& Mo, const Tabs& T) {
 }
 
 }  // namespace
+
+int cvd::ldsf_log2() {
+  const char* e = std::getenv("CVD_LDSF_LOG2");
+  return e && *e ? std::max(13, std::min(15, std::atoi(e))) : kLdsFilterLog2;
+}
+int64_t cvd::ldsf_max_rows() {
+  const char* e = std::getenv("CVD_LDSF_MAX_ROWS");
+  return e && *e ? (int64_t)std::atoll(e) : (kLdsFilterMaxRows << (ldsf_log2() - kLdsFilterLog2));
+}
 
 bool cvd::bitslice_preferred(const cvd_model& M) {
   const char* e = std::getenv("CVD_BITSLICE");

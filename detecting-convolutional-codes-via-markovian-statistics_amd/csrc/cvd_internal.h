@@ -50,6 +50,7 @@ struct cvd_model {
   // canonical digest hash, the directory of 256-B slots {six phase images, record}, and six
   // images per row by device row id
   bool bs = false;
+  int32_t bs_pat_bits = 12;       // pattern-table bits of the bit-sliced filter (the kernel's LDS table)
   int64_t bhcap = 0;
   int32_t bmax_probe = 0;
   std::vector<uint32_t> h_bfilt, h_bfilt_lds;   // [fcap] each (the LDS copy only with h_filt_lds)
@@ -127,6 +128,10 @@ bool walk_preferred(const cvd_model& M, bool early = false);
 // keys per two-word block, ~0.06% false positives) for 512-thread blocks, two per CU
 constexpr int kLdsFilterLog2 = 14;
 constexpr int64_t kLdsFilterMaxRows = 32768;
+// the LDS filter's size (2^log2 words) and row cap: kLdsFilterLog2 / kLdsFilterMaxRows unless
+// CVD_LDSF_LOG2 (13..15; 15: 128 KiB, 1,024-thread blocks) / CVD_LDSF_MAX_ROWS set them
+int ldsf_log2();
+int64_t ldsf_max_rows();
 bool ldsf_preferred(const cvd_model& M);
 int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
                     uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,

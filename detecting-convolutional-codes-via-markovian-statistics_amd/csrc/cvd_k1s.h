@@ -25,6 +25,12 @@ constexpr int kBsSlotShift = 6;      // directory slot: 64 dwords
 constexpr int kBsRecWord = 48;       // record r at dwords 48 + 4 r of a slot (images 8 x 6 before it)
 constexpr int kBsDkeyWords = 48;     // six images per row in a.dkey
 constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
+// timing ablation (CVD_JIT_DEFINES=-DCVD_K1S_ABL=1; results differ): the waves of H2
+// sequences read filter word 0 instead of their own and never take a candidate, so a launch
+// times the lockstep kernel without their random L2 requests
+#ifndef CVD_K1S_ABL
+#define CVD_K1S_ABL 0
+#endif
 
 // LDS: per (phase, y) two uint4 {e0, e1, ez, 0} of word 0 and word 1 (cvd::bs_eplanes)
 __device__ __forceinline__ uint4* bs_etab_lds() {
@@ -42,13 +48,26 @@ __device__ __forceinline__ void fill_bs_etab() {
 }
 
 // P̂1 row cursor over the bit-sliced tables (RowCursor's protocol: slot >= 0 known row id,
-// -1 known unvisited row, -2 pending hash probe)
+// -1 known unvisited row, -2 pending hash probe).  The lookup of D_t is issued AHEAD of the
+// resolve of D_{t-1} (hash_ahead, right after the ACS): every lane whose D_{t-1} row is not
+// known from a successor record (slot < 0) hashes D_t and reads its filter word before the
+// step waits for D_{t-1}'s key and record loads; the lanes whose D_{t-1} turns out to be a
+// row (a filter-positive candidate that matches) simply do not use it.  So the filter read
+// has the rest of the step and half of the next one to land, and the key and record loads
+// the second word's ACS plus the hash.
 struct BsCursor {
   int32_t slot, pnx;
-  uint32_t hs, fb, fw, fb1, fw1, pc;
+  uint32_t hs, hsn, fb, fw, fb1, fw1, pc;   // hs: home slot of D_{t-1}'s lookup, hsn: of D_t's
   bool cand;
+  bool h2wave = false;   // (CVD_K1S_ABL timing studies: the wave holds H2 sequences only)
   double plp;
   uint32_t pkey[8];
+  // two-step records (a.t2, lockstep lanes that walk learned rows): half 1 = plp / pnx hold the
+  // first step of a record whose second is plp2 / pnx2; half 2 = plp / pnx hold that second
+  // step, so the next step needs no load
+  double plp2;
+  int32_t pnx2;
+  uint32_t half;
   // entry rn (16 B {log P̂1, successor row, T_ref count c}) of learned row s, dense records
   __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
     uint32_t o;
@@ -58,19 +77,35 @@ struct BsCursor {
     pnx = (int32_t)v.z;
     plp = __hiloint2double((int)v.y, (int)v.x);
   }
-  __device__ void start(const ExpArgs& a, uint32_t r0) {
-    slot = a.slot0; hs = 0u; fb = 0u; fw = 0u; fb1 = 0u; fw1 = 0u; cand = false; pc = 1u;
-    prefetch_row(a, slot, r0);
+  // the two-step record (learned row s, words rn then rnn): {log P̂1 of both steps, row after
+  // one step + 1, row after two + 1} (cvd_host.cpp, t2)
+  __device__ void prefetch_t2(const ExpArgs& a, int32_t s, uint32_t rn, uint32_t rnn) {
+    const uint32_t* e = a.t2 + ((size_t)s * 16u + (rn | (rnn << 2))) * 8u;
+    const uint4 v = *reinterpret_cast<const uint4*>(e);
+    const uint2 w = *reinterpret_cast<const uint2*>(e + 4);
+    plp = __hiloint2double((int)v.y, (int)v.x);
+    plp2 = __hiloint2double((int)v.w, (int)v.z);
+    pnx = (int32_t)(w.x & 0x0FFFFFFFu) - 1;
+    pnx2 = (int32_t)(w.y & 0x0FFFFFFFu) - 1;
+    half = 1u;
+  }
+  __device__ void start(const ExpArgs& a, uint32_t r0, uint32_t r1) {
+    slot = a.slot0; hs = 0u; hsn = 0u; fb = 0u; fw = 0u; fb1 = 0u; fw1 = 0u; cand = false; pc = 1u; half = 0u;
+    plp2 = 0.0; pnx2 = -1;
+    if (a.t2) prefetch_t2(a, slot, r0, r1);
+    else prefetch_row(a, slot, r0);
   }
   // ordering fences (RowCursor::fence): the waits for the loads issued a step / half a step
-  // earlier land after the ACS work the dependency names
-  __device__ void fence(uint32_t dep) {
-    asm volatile("" : "+v"(fw), "+v"(fw1), "+v"(slot), "+v"(pnx), "+v"(plp) : "v"(dep));
+  // earlier land after the ACS work the dependency names.  fence_mid: the filter words (the
+  // candidate test); fence_resolve: the lookup state of D_{t-1} (its key, record, slot) --
+  // not the filter words hash_ahead has just requested
+  __device__ void fence_mid(uint32_t dep) {
+    asm volatile("" : "+v"(fw), "+v"(fw1), "+v"(slot) : "v"(dep));
   }
-  __device__ void fence_keys(uint32_t dep) {
+  __device__ void fence_resolve(uint32_t dep) {
+    asm volatile("" : "+v"(slot), "+v"(pnx), "+v"(plp), "+v"(pc), "+v"(pnx2), "+v"(plp2) : "v"(dep));
 #pragma unroll
     for (int w = 0; w < 8; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
-    asm volatile("" : "+v"(pc) : "v"(dep));
   }
   __device__ static const uint32_t* slot_ptr(const ExpArgs& a, uint32_t s) {
     return a.hkey + ((size_t)s << kBsSlotShift);
@@ -109,7 +144,8 @@ struct BsCursor {
   __device__ double resolve(const ExpArgs& a, const uint32_t (&R)[2][4], uint32_t r, double lpu) {
     double lpv = lpu;
     int32_t ns = -2;
-    if (slot >= 0) {
+    const bool known = slot >= 0;
+    if (known) {
       lpv = plp; ns = pnx;
     } else if (cand) {
       if (same(pkey, R)) {
@@ -134,30 +170,52 @@ struct BsCursor {
       }
     }
     slot = ns;
+    // a two-step record's second step (its row after one step is D_t's): ready for the next
+    if (known && half == 1u && ns >= 0) {
+      plp = plp2; pnx = pnx2; half = 2u;
+    } else {
+      half = 0u;
+    }
     return lpv;
   }
-  // D_t (planes N at phase PH) is known: issue the next step's loads (kRow: the dense
-  // record of a known row; walk mode loads its own)
-  template <int PH, bool kRow = true>
-  __device__ void prefetch(const ExpArgs& a, const uint32_t (&N)[2][4], uint32_t rn) {
-    if (slot >= 0) {
-      if (kRow) prefetch_row(a, slot, rn);
-    } else if (slot == -2) {
+  // D_t (planes N at phase PH) is known, D_{t-1}'s lookup not yet resolved: a lane whose
+  // D_{t-1} row is not known from a successor (slot < 0) may need D_t's lookup, so it hashes
+  // D_t and requests the filter word now
+  // (no divergent branch: a wave hashes whenever one lane needs it anyway, and a load under
+  // a divergent branch made the compiler's wait counts conservative -- it waited for this
+  // load at the resolve, vmcnt(0).  A lane that does not need the lookup reads filter word 0
+  // instead: every such lane of a wave shares that one L2 line; reading each lane's own
+  // block measured 26% slower at p = 0.05, where most H1 lanes walk their rows' successors)
+  template <int PH>
+  __device__ void hash_ahead(const ExpArgs& a, const uint32_t (&N)[2][4]) {
+    {
       uint32_t ph, pl;
       cvd::bs_digest_hash<PH>(N, ph, pl);
-      hs = ph & a.hmask;
+      hsn = ph & a.hmask;
       const uint2 pp = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(filter_patterns_lds()) +
                                                        (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 3)));
       fb = pp.x;
       fb1 = pp.y;
+      const uint32_t fo = slot < 0 && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & a.fmask4) : 0u;
 #if CVD_K1B_LDSF
-      const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + (pl & a.fmask4));
+      const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + fo);
 #else
-      const uint2 f = ld_off<uint2>(a.filt, pl & a.fmask4);
+      const uint2 f = ld_off<uint2>(a.filt, fo);
 #endif
       fw = f.x;
       fw1 = f.y;
+      if ((CVD_K1S_ABL & 1) && h2wave) { fw = 0u; fw1 = 0u; }
     }
+  }
+  // after the resolve: a known row's dense record for the next word (kRow; walk mode loads
+  // its own), and D_t's home slot becomes the pending lookup's
+  template <bool kRow = true>
+  __device__ void next(const ExpArgs& a, uint32_t rn, uint32_t rnn = 0u) {
+    if (kRow && slot >= 0 && half != 2u) {
+      if (a.t2) prefetch_t2(a, slot, rn, rnn);
+      else prefetch_row(a, slot, rn);
+    }
+    hs = hsn;
   }
 };
 
@@ -171,9 +229,11 @@ __device__ __forceinline__ void bs_step(const ExpArgs& a, BsCursor& cur, const u
   const uint32_t e0[2] = {E0.x, E1.x}, e1[2] = {E0.y, E1.y}, ez[2] = {E0.z, E1.z};
   uint32_t mu;
   cvd::bs_step_core<PH, kUni>(R, e0, e1, ez, N, mu, c, [&](uint32_t dep) {
-    cur.fence(dep);                  // dep: the first word's ACS result
+    cur.fence_mid(dep);              // dep: the first word's ACS result
     cur.template mid<PH>(a, rr);
   });
+  cur.template hash_ahead<(PH + 1) % 6>(a, N);   // D_t's filter read before D_{t-1}'s loads are waited for
+  cur.fence_resolve(N[1][3]);        // N[1][3] depends on the whole ACS
 }
 
 // H1 waves in walk mode (k1b_walk's schedule; the planes' layout phase is the wave's)
@@ -202,8 +262,8 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   uint32_t R[2][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
   double lp = 0.0, lr = 0.0;
   BsCursor cur;
-  cur.slot = -1; cur.pnx = -1; cur.hs = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u;
-  cur.cand = false; cur.plp = 0.0; cur.pc = 1u;
+  cur.slot = -1; cur.pnx = -1; cur.hs = 0u; cur.hsn = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u;
+  cur.cand = false; cur.plp = 0.0; cur.pc = 1u; cur.half = 0u; cur.plp2 = 0.0; cur.pnx2 = -1;
   double plp2 = 0.0;
   auto two_steps = [&]() -> bool { return a.t2 != nullptr && pos + 2u <= N; };
   auto walk_prefetch = [&]() {
@@ -242,20 +302,16 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
     uint32_t Nn[2][4], c;
     bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
     if (mode == kWalkAcs) {
-      cur.fence(Nn[1][3]);
-      cur.fence_keys(Nn[1][3]);
       lp += cur.template resolve<PH>(a, R, rr, a.lp_unseen);   // Pd_plotter.py:115, T = P̂1
       lr += s_lt[c];                                            // Pd_plotter.py:115, T = T_ref(1/2)
       advance();
+      cur.template next<false>(a, 0u);
       if (finished()) {
         mode = kWalkDone;
         cur.slot = -1;
-      } else {
-        cur.template prefetch<(PH + 1) % 6, false>(a, Nn, word_at() & 3u);   // hashed lookups
-        if (cur.slot >= 0) {
-          mode = kWalkWalk;
-          walk_prefetch();
-        }
+      } else if (cur.slot >= 0) {
+        mode = kWalkWalk;
+        walk_prefetch();
       }
     }
 #pragma unroll
@@ -413,31 +469,30 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
     int64_t wi = 0;
     uint32_t sh = 0u;
     BsCursor cur;
-    cur.start(a, cw & 3u);
-    auto step = [&](auto phc, uint32_t rr, uint32_t rn) {
+    cur.start(a, cw & 3u, (cw >> 2) & 3u);
+    if (CVD_K1S_ABL & 1) cur.h2wave = hmask == 0u;
+    auto step = [&](auto phc, uint32_t rr, uint32_t rn, uint32_t rnn) {
       constexpr int PH = decltype(phc)::value;
       uint32_t Nn[2][4], c;
       bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
-      cur.fence(Nn[1][3]);                       // Nn[1][3] depends on the whole ACS
-      cur.fence_keys(Nn[1][3]);
       lp += cur.template resolve<PH>(a, R, rr, lpu);   // Pd_plotter.py:115, T = P̂1
       lr += s_lt[c];                                   // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
         for (int i = 0; i < 4; ++i) R[r][i] = Nn[r][i];
-      cur.template prefetch<(PH + 1) % 6>(a, R, rn);
+      cur.next(a, rn, rnn);
     };
     int64_t t = 0;
     int grp = 0, dec = 0;
     for (; t + 6 <= N; t += 6) {
       const uint32_t win = __builtin_amdgcn_alignbit(nw, cw, sh);
-      step(IntC<0>{}, bits2(win, 0), bits2(win, 2));
-      step(IntC<1>{}, bits2(win, 2), bits2(win, 4));
-      step(IntC<2>{}, bits2(win, 4), bits2(win, 6));
-      step(IntC<3>{}, bits2(win, 6), bits2(win, 8));
-      step(IntC<4>{}, bits2(win, 8), bits2(win, 10));
-      step(IntC<5>{}, bits2(win, 10), bits2(win, 12));
+      step(IntC<0>{}, bits2(win, 0), bits2(win, 2), bits2(win, 4));
+      step(IntC<1>{}, bits2(win, 2), bits2(win, 4), bits2(win, 6));
+      step(IntC<2>{}, bits2(win, 4), bits2(win, 6), bits2(win, 8));
+      step(IntC<3>{}, bits2(win, 6), bits2(win, 8), bits2(win, 10));
+      step(IntC<4>{}, bits2(win, 8), bits2(win, 10), bits2(win, 12));
+      step(IntC<5>{}, bits2(win, 10), bits2(win, 12), bits2(win, 14));
       sh += 12u;
       if (sh >= 32u) {
         sh -= 32u;
@@ -458,11 +513,11 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
     // last 1-5 steps
     if (t < N) {
       const uint32_t win = __builtin_amdgcn_alignbit(nw, cw, sh);
-      step(IntC<0>{}, bits2(win, 0), bits2(win, 2));
-      if (t + 1 < N) step(IntC<1>{}, bits2(win, 2), bits2(win, 4));
-      if (t + 2 < N) step(IntC<2>{}, bits2(win, 4), bits2(win, 6));
-      if (t + 3 < N) step(IntC<3>{}, bits2(win, 6), bits2(win, 8));
-      if (t + 4 < N) step(IntC<4>{}, bits2(win, 8), bits2(win, 10));
+      step(IntC<0>{}, bits2(win, 0), bits2(win, 2), bits2(win, 4));
+      if (t + 1 < N) step(IntC<1>{}, bits2(win, 2), bits2(win, 4), bits2(win, 6));
+      if (t + 2 < N) step(IntC<2>{}, bits2(win, 4), bits2(win, 6), bits2(win, 8));
+      if (t + 3 < N) step(IntC<3>{}, bits2(win, 6), bits2(win, 8), bits2(win, 10));
+      if (t + 4 < N) step(IntC<4>{}, bits2(win, 8), bits2(win, 10), bits2(win, 12));
     }
     if (a.sums) {
       const int64_t qe = qwave + lane_id();

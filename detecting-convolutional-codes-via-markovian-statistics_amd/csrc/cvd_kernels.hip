@@ -1695,8 +1695,8 @@ static int env_i(const char* name, int def) {
 // threads with the global filter 570.9 / 668.7, 512 threads 541.6 / 625.7).  CVD_NO_LDSF=1
 // keeps the filter in global memory.
 bool cvd::ldsf_preferred(const cvd_model& M) {
-  return !std::getenv("CVD_NO_LDSF") && walk_preferred(M) && M.n_rows <= kLdsFilterMaxRows &&
-         M.fcap <= ((int64_t)1 << kLdsFilterLog2) && M.h_filt_lds.size() == (size_t)M.fcap;
+  return !std::getenv("CVD_NO_LDSF") && walk_preferred(M) && M.n_rows <= ldsf_max_rows() &&
+         M.fcap <= ((int64_t)1 << ldsf_log2()) && M.h_filt_lds.size() == (size_t)M.fcap;
 }
 
 bool cvd::walk_preferred(const cvd_model& M, bool early) {
@@ -1850,15 +1850,17 @@ int cvd::upload_model(cvd_model& M, int device) {
   M.rtc_ldsf = M.k1b_ok && M.hcap > 0 && ldsf_preferred(M);
   // block size: 512 threads with the LDS filter (two blocks of 8 waves per CU hold it),
   // else 256 (CVD_K1B_BLOCK=256/512/1024 overrides, timing studies)
-  M.rtc_block = env_i("CVD_K1B_BLOCK", M.rtc_ldsf ? 512 : kBlock);
+  M.rtc_block = env_i("CVD_K1B_BLOCK", M.rtc_ldsf ? (M.fcap > ((int64_t)1 << 14) ? 1024 : 512) : kBlock);
   if (M.rtc_block != 256 && M.rtc_block != 512 && M.rtc_block != 1024) M.rtc_block = kBlock;
   // the bit-sliced form (k1s) for models with the bit-sliced tables; if it cannot be
   // built, the butterfly kernel on the nibble tables
   M.rtc_bs = false;
   for (int attempt = M.bs && M.d_bkey ? 0 : 1; attempt < 2 && M.k1b_ok && M.hcap > 0; ++attempt) {
     const bool bs = attempt == 0;
+    const int patbits = M.rtc_ldsf ? kFilterPatBitsLds : bs ? M.bs_pat_bits : kFilterPatBits;
     const std::string vdefs = "-DCVD_K1B_BLOCK=" + std::to_string(M.rtc_block) +
-                              (M.rtc_ldsf ? " -DCVD_K1B_LDSF=1 -DCVD_FILTER_PAT_BITS=" + std::to_string(kFilterPatBitsLds) : "") +
+                              (M.rtc_ldsf ? " -DCVD_K1B_LDSF=1" : "") +
+                              (patbits != kFilterPatBits ? " -DCVD_FILTER_PAT_BITS=" + std::to_string(patbits) : "") +
                               (bs ? " -DCVD_K1B_BITSLICE=1" : "");
     if (rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn, &M.rtc_fn_multi) == 0) {
       M.rtc_bs = bs;
@@ -1974,7 +1976,8 @@ static bool multi_ok(const cvd_model& M) {
 }
 static bool multi_same(const cvd_model& A, const cvd_model& B) {
   return A.rtc_fn_multi == B.rtc_fn_multi && A.rtc_block == B.rtc_block && A.rtc_ldsf == B.rtc_ldsf &&
-         A.rtc_bs == B.rtc_bs && A.device == B.device && (!A.rtc_ldsf || A.fcap == B.fcap);
+         A.rtc_bs == B.rtc_bs && (!A.rtc_bs || A.bs_pat_bits == B.bs_pat_bits) && A.device == B.device &&
+         (!A.rtc_ldsf || A.fcap == B.fcap);
 }
 // the same criterion as one id (cvd_model_info.multi_variant: the Python host groups launches
 // for per-launch timing by it): equal for models multi_same merges, 0 if multi_ok fails

@@ -163,13 +163,15 @@ def main(src, name):
         import isa_breakdown
         import valu_model
         import tempfile
+        bs = "bit-sliced" in out["kernel"]    # k1s: six steps per loop trip (isa_breakdown)
         with tempfile.TemporaryDirectory() as d:
-            lines = isa_breakdown.build_isa(out["config"], [], os.path.join(d, "k.s"))
+            lines = isa_breakdown.build_isa(out["config"], ["-DCVD_K1B_BITSLICE=1"] if bs else [],
+                                            os.path.join(d, "k.s"))
         mix = {}
-        for _name, ins in isa_breakdown.blocks(isa_breakdown.main_loop(lines)):
+        for _name, ins in isa_breakdown.blocks(isa_breakdown.main_loop(lines, 1 if bs else 0)):
             for x in ins:
                 if x.startswith("v_"):
-                    mix[x.split()[0]] = mix.get(x.split()[0], 0) + 0.25    # 4 steps per loop trip
+                    mix[x.split()[0]] = mix.get(x.split()[0], 0) + (1 / 6 if bs else 0.25)
         cyc, by = valu_model.load_cycles()
         avg, by_class = valu_model.weighted_cycles(mix, cyc)
         out["valu_cycles_per_inst"] = avg

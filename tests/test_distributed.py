@@ -79,3 +79,40 @@ def test_sharded_counts_equal_single_process(pkg, tmp_path, world):
             mod = C.Model(c1, p, None, 200, 1.0, 7)
             cnt, _ = mod.run_trials(c1, c2, N, p, 7, 0, 101, nthreads=2)
             assert got[iN, ip].tolist() == cnt.tolist()
+
+
+def _reduce_worker(rank, world, port, out_path):
+    """bench.reduce_record on gloo ranks: the true reduce passes, a corrupted one raises."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    shard = torch.tensor([[rank + 1, 10 * rank], [7, rank]], dtype=torch.int64)
+    red = shard.clone()
+    dist.all_reduce(red)
+    rec = bench.reduce_record(dist, shard, red, world, rank, "test")
+    bad = red.clone()
+    bad[0, 0] += 1                      # a reduce that lost or doubled a shard
+    try:
+        bench.reduce_record(dist, shard, bad, world, rank, "test")
+        raised = False
+    except RuntimeError:
+        raised = True
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump({"rec": rec, "raised": raised, "red": red.tolist()}, f)
+    dist.destroy_process_group()
+
+
+def test_bench_reduce_record_checks_the_reduce(tmp_path):
+    import json
+    out = str(tmp_path / "rec.json")
+    mp.start_processes(_reduce_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    got = json.load(open(out))
+    rec = got["rec"]
+    assert rec["world_size"] == 2 and rec["backend"] == "gloo" and rec["shards_sum_equals_reduced"]
+    assert rec["rank_shards"] == [[[1, 0], [7, 0]], [[2, 10], [7, 1]]]
+    assert got["red"] == [[3, 10], [14, 1]]
+    assert got["raised"]
