@@ -648,16 +648,24 @@ def run_c4(a, pkg, world, rank, local, dist):
     # residency rounds (393,216 trials, 197 GB) instead of two
     budget = min(int(free * 0.75), 200 << 30)
 
-    def batch_of(N):
-        b = det.default_batch(N, hi - lo, budget)
+    def batch_of(N, slots=1):
+        # slots: stream slots the call holds at once (a p row in one cvd_mc_run_grid call: one
+        # per p), so that the call's whole workspace, not one slot, fits the budget
+        b = det.default_batch(N, hi - lo, budget // slots)
         return max(1, b)
+
+    def row_call(N):
+        return N < 100_000       # the whole p row of this N in one grid call (below)
 
     counts = torch.zeros((len(Ns), len(p_grid), 2), dtype=torch.int64, device=det.device)
     # the largest stream workspace, allocated once before the timed region and left in
     # torch's caching allocator, so no grid call inside it pays a fresh ~200 GB hipMalloc
     # (N = 1e5's first point took 7.4 s instead of 3.4 s that way, profiles/r04j/)
     g1c = pkg.Code(cc["gen1"], m, k, n)
-    ws = max(pkg.lib().cvd_mc_workspace_bytes(g1c.c, N, batch_of(N)) for N in Ns)
+    from dccvm_amd.detector import grid_workspace_bytes
+    mlist = [models[p] for p in p_grid]
+    ws = max(grid_workspace_bytes(mlist, g1c, [N], batch_of(N, len(p_grid)), 0) if row_call(N)
+             else pkg.lib().cvd_mc_workspace_bytes(g1c.c, N, batch_of(N)) for N in Ns)
     del_me = torch.empty(max(ws, 4) // 4, dtype=torch.int32, device=det.device)
     del del_me
     # warmup: one small launch per p (smallest N) at trial ids far from the timed ones
@@ -670,22 +678,21 @@ def run_c4(a, pkg, world, rank, local, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    mlist = [models[p] for p in p_grid]
     for iN, N in enumerate(Ns):
         tn = time.perf_counter()
-        B = batch_of(N)
-        if N >= 100_000:
+        B = batch_of(N, len(p_grid)) if row_call(N) else batch_of(N)
+        if not row_call(N):
             # a progress line per long grid point (the launches are queued): one grid call per p
             for ip, p in enumerate(p_grid):
                 det.run_grid([models[p]], cc["gen1"], cc["gen2"], [p], [N], a.seed, lo, hi, batch=B,
-                             counts=counts[iN, ip].view(1, 1, 2))
+                             counts=counts[iN, ip].view(1, 1, 2), budget=budget)
                 torch.cuda.synchronize()
                 print(json.dumps({"c4_point": {"rank": rank, "N": N, "p": p, "seconds": time.perf_counter() - tn}}),
                       file=sys.stderr, flush=True)
         else:
             # the whole p row of this N in ONE library call (cvd_mc_run_grid)
             det.run_grid(mlist, cc["gen1"], cc["gen2"], p_grid, [N], a.seed, lo, hi, batch=B,
-                         counts=counts[iN].view(1, len(p_grid), 2))
+                         counts=counts[iN].view(1, len(p_grid), 2), budget=budget)
         torch.cuda.synchronize()
         per_n_s.append(time.perf_counter() - tn)
         print(json.dumps({"c4_progress": {"rank": rank, "N": N, "seconds": per_n_s[-1]}}), file=sys.stderr,
@@ -716,7 +723,7 @@ def run_c4(a, pkg, world, rank, local, dist):
         # the N's whole pipeline time (generator + detector, max over ranks)
         ab = T * len(p_grid) * 2 * ((N * n + 7) // 8)
         ach = ab / per_n_s[i] / 1e9
-        b = batch_of(N)
+        b = batch_of(N, len(p_grid)) if row_call(N) else batch_of(N)
         lpp = -(-(hi - lo) // b)                          # launches per grid point on a rank
         return {"algorithmic_bytes": ab, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": ach / HBM_PEAK_GBS, "basis": "whole pipeline time of this N (generator + detector)",
@@ -726,7 +733,8 @@ def run_c4(a, pkg, world, rank, local, dist):
 
     per_N = {str(N): {"trials": T * len(p_grid), "seconds": per_n_s[i], "trials_per_s": T * len(p_grid) / per_n_s[i],
                       "seq_steps_per_s": 2 * T * len(p_grid) * N / per_n_s[i],
-                      "batch_per_rank": batch_of(N), "roofline": roof_N(i, N),
+                      "batch_per_rank": batch_of(N, len(p_grid)) if row_call(N) else batch_of(N),
+                      "roofline": roof_N(i, N),
                       "per_p": {str(p): {"h1_successes": int(c[i, j, 0]), "h2_successes": int(c[i, j, 1]),
                                          "Pd": float(c[i, j, 0]) / T, "Pc": float(c[i, j, 0] + c[i, j, 1]) / (2 * T)}
                                 for j, p in enumerate(p_grid)}}

@@ -736,6 +736,11 @@ enum : uint32_t { kWalkAcs = 0u, kWalkPend = 1u, kWalkWalk = 2u, kWalkDone = 3u 
 #ifndef CVD_WALK_ABL
 #define CVD_WALK_ABL 0
 #endif
+// the walk loop's guard bound, iterations per step of N (tests: CVD_JIT_DEFINES=-DCVD_WALK_GUARD=0
+// trips it at once, so the error flag's path is exercised)
+#ifndef CVD_WALK_GUARD
+#define CVD_WALK_GUARD 128
+#endif
 
 template <int m, uint64_t XM>
 __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64_t vmask, const double* s_lt) {
@@ -886,7 +891,7 @@ __device__ __forceinline__ void k1b_walk(const ExpArgs& a, int64_t qwave, uint64
   // every iteration moves a lane a step or out of a walk: 2 (N + 1) per lane bound it
   // (a guard only: the loop ends by itself)
   int64_t st_acs = 0, st_burst = 0, st_biter = 0, st_unpack = 0, st_lanes_acs = 0, st_lanes_walk = 0;
-  for (int64_t it = 0, it_max = 128 * ((int64_t)N + 1); it < it_max; ++it) {
+  for (int64_t it = 0, it_max = CVD_WALK_GUARD * ((int64_t)N + 1); it < it_max; ++it) {
     if (need) {
       nxtw = load_word((pos >> 4) + 1u);
       need = false;

@@ -321,7 +321,7 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   };
   const uint32_t wmin = (uint32_t)a.walk_wmin, amin = (uint32_t)a.walk_amin;
   const int burst = a.walk_burst;
-  for (int64_t it = 0, it_max = 128 * ((int64_t)N + 1); it < it_max; ++it) {
+  for (int64_t it = 0, it_max = CVD_WALK_GUARD * ((int64_t)N + 1); it < it_max; ++it) {
     if (need) {
       nxtw = load_word((pos >> 4) + 1u);
       need = false;

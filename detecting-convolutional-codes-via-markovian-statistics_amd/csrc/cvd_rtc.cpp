@@ -280,9 +280,14 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(device);
     hipModule_t mod;
-    const bool loaded = hipModuleLoadData(&mod, code.data()) == hipSuccess &&
-                        hipModuleGetFunction(&fn, mod, "cvd_k1b_spec") == hipSuccess &&
-                        hipModuleGetFunction(&fnm, mod, "cvd_k1b_spec_multi") == hipSuccess;
+    bool loaded = hipModuleLoadData(&mod, code.data()) == hipSuccess;
+    if (loaded && hipModuleGetFunction(&fn, mod, "cvd_k1b_spec") != hipSuccess) {
+      (void)hipModuleUnload(mod);   // no single-model entry: the module is of no use
+      loaded = false;
+    }
+    // without the multi-model entry the model still runs the specialised kernel, one launch
+    // per model (multi_ok checks rtc_fn_multi)
+    if (loaded && hipModuleGetFunction(&fnm, mod, "cvd_k1b_spec_multi") != hipSuccess) fnm = nullptr;
     (void)hipSetDevice(cur);
     return loaded;
   };

@@ -368,14 +368,20 @@ class Detector:
 
     def run_trials(self, model, gen1, gen2, N, p, seed, trial_begin, trial_end, batch=None,
                    path=_lib.PATH_AUTO, return_sums=False, counts=None, stream=None, early_decision=False,
-                   fused=False):
+                   fused=False, check=None):
         """Global trials [trial_begin, trial_end) of one (N, p) grid point
         (Pd_plotter.py:198-223).  Returns {"counts": (s1, s2), "sums": [T, 4]?}
         with sums per trial = (logp1, logp1_ref, logp2, logp2_ref).
         early_decision (counts only): stop each trial once its decision is certain.
         fused: generator and table automaton in one kernel (cvd_mc_fused; dense
         LDS-resident models), sums included; the counts-only path uses it on its own
-        (cvd_mc_run, PATH_AUTO) whenever it applies."""
+        (cvd_mc_run, PATH_AUTO) whenever it applies.
+        check: read the model's kernel error flags afterwards (cvd_model_device_error,
+        which synchronises) and raise if a launch set one; default: when sums are returned
+        (the call synchronises anyway), not for counts-only calls, whose caller checks once
+        after its launches (model.device_error())."""
+        if check is None:
+            check = return_sums
         if early_decision and return_sums:
             raise ValueError("early_decision gives counts only; per-trial sums need the full run")
         g1 = as_code(gen1, self.m, self.k, self.n)
@@ -392,6 +398,8 @@ class Detector:
                                                int(seed) & 0xFFFFFFFFFFFFFFFF, int(trial_begin), int(trial_end),
                                                ctypes.c_void_p(sums.data_ptr() if sums is not None else 0),
                                                ctypes.c_void_p(counts.data_ptr()), flags, _stream_ptr(stream)))
+            if check:
+                model.device_error()
             if return_sums:
                 return {"counts": counts, "sums": sums.cpu().numpy()}
             return {"counts": counts}
@@ -409,6 +417,8 @@ class Detector:
                                       int(seed) & 0xFFFFFFFFFFFFFFFF, int(trial_begin), int(trial_end),
                                       batch, ctypes.c_void_p(work.data_ptr() if work is not None else 0),
                                       ctypes.c_void_p(counts.data_ptr()), int(path) | flags, _stream_ptr(stream)))
+            if check:
+                model.device_error()
             return {"counts": counts}
         tag = grid_tag(N, p)
         out = []
@@ -421,14 +431,21 @@ class Detector:
             self.detect(model, r, N, 2 * Tb, Tb, sums=sums, counts=counts, path=path, stream=stream)
             s = sums.cpu().numpy()
             out.append(np.concatenate([s[:Tb], s[Tb:]], axis=1))
+        if check:
+            model.device_error()
         return {"counts": counts, "sums": np.concatenate(out, axis=0)}
 
 
     def run_grid(self, models, gen1, gen2, p_list, N_list, seed, trial_begin, trial_end, batch=None,
-                 path=_lib.PATH_AUTO, counts=None, stream=None, early_decision=False):
+                 path=_lib.PATH_AUTO, counts=None, stream=None, early_decision=False, budget=None):
         """The (N, p) grid of Pd_plotter.py:196-233 in ONE library call (cvd_mc_run_grid,
         SURVEY.md §8(b)): models[i] learned at p_list[i]; global trials [trial_begin,
-        trial_end) at every point; returns the int64 counts [len(N_list), len(p_list), 2]."""
+        trial_end) at every point; returns the int64 counts [len(N_list), len(p_list), 2].
+
+        `batch` is trials per launch PER GRID POINT of a p row: the p row's batches are
+        generated into one stream slot each, so the workspace is about len(p_list) times one
+        point's.  An explicit batch is clamped so that the workspace stays within `budget`
+        bytes (default: the free-memory budget batch=None uses; clamp_grid_batch)."""
         g1 = as_code(gen1, self.m, self.k, self.n)
         g2 = as_code(gen2, self.m, self.k, self.n)
         npn, nN = len(p_list), len(N_list)
@@ -439,15 +456,18 @@ class Detector:
         T = int(trial_end) - int(trial_begin)
         if T <= 0:
             return counts
+        if budget is None:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            budget = min(free // 3, 96 << 30)
         if batch is None:
             # the p row's batches share the HBM budget (one stream slot per point)
-            free, _ = torch.cuda.mem_get_info(self.device)
-            batch = self.default_batch(max(N_list), T, min(free // 3, 96 << 30) // max(1, npn))
+            batch = self.default_batch(max(N_list), T, budget // max(1, npn))
         hs = (ctypes.c_void_p * npn)(*[m.handle.value for m in models])
         pv = (ctypes.c_double * npn)(*[float(p) for p in p_list])
         Nv = (ctypes.c_int64 * nN)(*[int(N) for N in N_list])
         lib = _lib.lib()
         flags = _lib.DETECT_EARLY_DECISION if early_decision else 0
+        batch = clamp_grid_batch(models, g1, N_list, batch, int(path) | flags, budget)
         wsz = lib.cvd_mc_grid_workspace_bytes(hs, npn, g1.c, Nv, nN, batch, int(path) | flags)
         if wsz < 0:
             raise _lib.CvdError("cvd_mc_grid_workspace_bytes: bad arguments")
@@ -457,6 +477,27 @@ class Detector:
                                        ctypes.c_void_p(work.data_ptr() if work is not None else 0),
                                        ctypes.c_void_p(counts.data_ptr()), int(path) | flags, _stream_ptr(stream)))
         return counts
+
+
+def grid_workspace_bytes(models, g1, N_list, batch, flags):
+    """cvd_mc_grid_workspace_bytes of a p row of `models` (host call, no GPU needed)."""
+    npn, nN = len(models), len(N_list)
+    hs = (ctypes.c_void_p * npn)(*[m.handle.value for m in models])
+    Nv = (ctypes.c_int64 * nN)(*[int(N) for N in N_list])
+    wsz = _lib.lib().cvd_mc_grid_workspace_bytes(hs, npn, g1.c, Nv, nN, int(batch), int(flags))
+    if wsz < 0:
+        raise _lib.CvdError("cvd_mc_grid_workspace_bytes: bad arguments")
+    return int(wsz)
+
+
+def clamp_grid_batch(models, g1, N_list, batch, flags, budget):
+    """The largest batch <= `batch` whose grid workspace (one stream slot per p of the row)
+    fits `budget` bytes (at least 1 trial): the per-point batch a caller gives would
+    otherwise cost len(models) times its slot."""
+    batch = max(1, int(batch))
+    while batch > 1 and grid_workspace_bytes(models, g1, N_list, batch, flags) > budget:
+        batch = max(1, batch * budget // max(1, grid_workspace_bytes(models, g1, N_list, batch, flags)) - 1)
+    return batch
 
 
 # ───────────────────── reference-mirroring functions ────────────────────────

@@ -268,7 +268,10 @@ int cvd_mc_run_grid(const cvd_model* const* models, const cvd_code* enc1, const 
 /* Kernel error flags of a model's launches since the last call (synchronises its
  * device): bit 0 = a walk-mode wave (k1b_walk) left its scheduler loop by the guard
  * bound with lanes unfinished, so that launch's counts and sums are void.  Returns
- * CVD_E_STATE when any flag is set (then cleared), CVD_OK otherwise. */
+ * CVD_E_STATE when any flag is set (then cleared), CVD_OK otherwise.  cvd_detect,
+ * cvd_detect_multi, cvd_mc_run and cvd_mc_run_grid do not synchronise, so they cannot
+ * report it: a caller checks it once after its launches (the Python host does after
+ * run_trials with sums, run_grid, detect_multi's callers, run_experiment and the bench). */
 int cvd_model_device_error(cvd_model* model, int32_t* flags_out);
 
 /* The same grid point in ONE kernel per launch, without streams in HBM: every lane

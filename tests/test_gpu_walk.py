@@ -159,3 +159,17 @@ def test_lds_filter_model_under_jit_fallbacks(pkg, monkeypatch, how):
     got, gc = _sums(det, alt, cc, N, p, t0, t1)
     assert np.array_equal(got, ref)
     assert gc == rc
+
+
+def test_walk_guard_flag_is_reported(pkg, monkeypatch):
+    """The walk loop's guard (never reached in a correct schedule) sets the model's error
+    flag; a kernel built with a zero guard bound trips it at once, and run_trials (sums)
+    raises instead of returning void counts."""
+    cc = pkg.CONFIG_CODES["m6"]
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    monkeypatch.setenv("CVD_JIT_DEFINES", "-DCVD_WALK_GUARD=0")
+    model = pkg.Model(det.dec, 0.01, 300_000, 200, 1.0, 7).upload(0)
+    assert model.info()["walk"] == 1
+    with pytest.raises(pkg.CvdError, match="scheduler guard"):
+        det.run_trials(model, cc["gen1"], cc["gen2"], 2000, 0.01, 7, 0, 256, return_sums=True)
+    assert model.device_error() == 0          # the flag was read and cleared

@@ -187,3 +187,20 @@ def test_explicit_kernel_selection(pkg, golden, name, kernel):
     mod = pkg.Model(pkg.Code(taps, m, k, n), 0.05, 5000, 200, 1.0, 7, enum_cap=100)
     assert mod.info()["explicit_kernel"] == kernel
     assert kernel in pkg.KERNEL_NAMES
+
+
+def test_explicit_grid_batch_is_clamped_to_the_budget(pkg):
+    """run_grid's `batch` is per grid point and the p row holds one stream slot per point
+    (ADVICE r04): an explicit batch is clamped so that the whole row's workspace fits the
+    budget, and a batch that fits is kept."""
+    from dccvm_amd.detector import clamp_grid_batch, grid_workspace_bytes
+    cc = pkg.CONFIG_CODES["m6"]
+    g1 = pkg.Code(cc["gen1"], 6, 1, 2)
+    models = [pkg.Model(g1, p, 5000, 200, 1.0, 7) for p in (0.05, 0.1, 0.2)]
+    N_list = [100_000]
+    one = grid_workspace_bytes(models[:1], g1, N_list, 1000, 0)
+    row = grid_workspace_bytes(models, g1, N_list, 1000, 0)
+    assert row == 3 * one > 0
+    b = clamp_grid_batch(models, g1, N_list, 1000, 0, row // 2)
+    assert 1 <= b < 1000 and grid_workspace_bytes(models, g1, N_list, b, 0) <= row // 2
+    assert clamp_grid_batch(models, g1, N_list, 1000, 0, row) == 1000
