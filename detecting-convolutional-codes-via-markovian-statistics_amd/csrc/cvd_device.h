@@ -175,6 +175,7 @@ struct ExpArgs {
   int32_t walk_wmin, walk_amin, walk_burst;   // k1b_walk schedule (see there)
   double lt_min, lp_min;    // smallest log T_ref / log P̂1 increments (early_decide)
   int32_t* err;             // error flags (nullable): bit 0 = k1b_walk left its loop by the guard
+  const uint32_t* pf;       // k1s LDS pre-filter (CVD_K1S_PF): 2^kBsPfLog2Bits bits, copied into dynamic LDS
 };
 
 // Received words of one sequence, one word of lookahead (the next step's r is

@@ -605,19 +605,31 @@ void build_hash(cvd_model& Mo) {
   // per row whatever the lane's layout phase); a directory slot holds the row's image at
   // each of the six phases (the exact compare) and its record; a.dkey the six images by
   // device row id (walk mode).  Load <= 1/8 by default (CVD_BS_LOAD_LOG2): 256-B slots, so
-  // the directory stays within 2 GiB at 10^6 rows; offsets into it are 64-bit.
+  // the directory stays within 2 GiB at 10^6 rows; the kernel addresses it by 32-bit byte offsets.
   Mo.bs = bitslice_preferred(Mo);
-  Mo.h_bfilt.clear(); Mo.h_bfilt_lds.clear(); Mo.h_bkey.clear(); Mo.h_bdkey.clear();
+  int bload = 3;
+  if (const char* e = std::getenv("CVD_BS_LOAD_LOG2")) bload = std::max(1, std::min(5, std::atoi(e)));
+  int64_t bcap = 64;
+  while (bcap < ((int64_t)1 << bload) * Mo.n_rows) bcap <<= 1;
+  // the kernel addresses the directory, the two-step records and the images by 32-bit byte
+  // offsets: past 4 GiB (over ~2·10^6 rows) the model keeps the nibble tables
+  if (bcap * 256 > ((int64_t)1 << 32) || Mo.n_rows * 512 > ((int64_t)1 << 32)) Mo.bs = false;
+  Mo.h_bfilt.clear(); Mo.h_bfilt_lds.clear(); Mo.h_bkey.clear(); Mo.h_bdkey.clear(); Mo.h_bpf.clear();
   Mo.bhcap = 0; Mo.bmax_probe = 0;
   if (Mo.bs) {
-    int bload = 3;
-    if (const char* e = std::getenv("CVD_BS_LOAD_LOG2")) bload = std::max(1, std::min(5, std::atoi(e)));
     // the filter's pattern table (kernel LDS: 8 B per pattern pair); CVD_BS_PAT_BITS 8..12
     Mo.bs_pat_bits = kFilterPatBits;
     if (const char* e = std::getenv("CVD_BS_PAT_BITS")) Mo.bs_pat_bits = std::max(8, std::min(kFilterPatBits, std::atoi(e)));
+    // the LDS pre-filter (a 1,024-thread block holds it beside the pattern table, which then
+    // has 1,024 pairs)
+    const bool bpf = bs_pf_preferred(Mo, ldsf);
+    if (bpf) {
+      Mo.bs_pat_bits = std::min(Mo.bs_pat_bits, (int32_t)kFilterPatBitsLds);
+      Mo.bs_pf_log2 = kBsPfLog2Bits;
+      if (const char* e = std::getenv("CVD_BS_PF_LOG2")) Mo.bs_pf_log2 = std::max(16, std::min(20, std::atoi(e)));
+      Mo.h_bpf.assign((size_t)1 << (Mo.bs_pf_log2 - 5), 0u);
+    }
     const unsigned bnpat = 1u << Mo.bs_pat_bits;
-    int64_t bcap = 64;
-    while (bcap < ((int64_t)1 << bload) * Mo.n_rows) bcap <<= 1;
     Mo.bhcap = bcap;
     constexpr int kSlotW = 64, kRecW = 48, kImgW = 48;
     Mo.h_bkey.assign((size_t)bcap * kSlotW, 0u);   // c = 0 in every record: empty
@@ -641,6 +653,10 @@ void build_hash(cvd_model& Mo) {
         const unsigned nl = 1u << kFilterPatBitsLds;
         Mo.h_bfilt_lds[2 * fb] |= filter_pattern(filter_pattern_index(ph, nl));
         Mo.h_bfilt_lds[2 * fb + 1] |= filter_pattern_hi(filter_pattern_index(ph, nl), nl);
+      }
+      if (bpf) {
+        const uint32_t b = pl >> (32 - Mo.bs_pf_log2);
+        Mo.h_bpf[b >> 5] |= 1u << (b & 31u);
       }
       uint64_t slot = ph & (uint64_t)(bcap - 1);
       int probe = 0;
@@ -773,6 +789,12 @@ int cvd::ldsf_log2() {
 int64_t cvd::ldsf_max_rows() {
   const char* e = std::getenv("CVD_LDSF_MAX_ROWS");
   return e && *e ? (int64_t)std::atoll(e) : (kLdsFilterMaxRows << (ldsf_log2() - kLdsFilterLog2));
+}
+
+bool cvd::bs_pf_preferred(const cvd_model& M, bool ldsf) {
+  const char* e = std::getenv("CVD_BS_PF");
+  if (e && e[0] == '0') return false;
+  return M.bs && !ldsf;
 }
 
 bool cvd::bitslice_preferred(const cvd_model& M) {

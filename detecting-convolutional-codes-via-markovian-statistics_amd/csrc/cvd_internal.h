@@ -56,6 +56,11 @@ struct cvd_model {
   std::vector<uint32_t> h_bfilt, h_bfilt_lds;   // [fcap] each (the LDS copy only with h_filt_lds)
   std::vector<uint32_t> h_bkey;   // [bhcap][64]: images 8 words x 6 phases, records 4 x 4 (c = 0: empty)
   std::vector<uint32_t> h_bdkey;  // [n_rows][48]
+  // LDS pre-filter of k1s (CVD_K1S_PF): one bit per row at bit pl >> (32 - kBsPfLog2Bits) of
+  // its digest hash, 2^kBsPfLog2Bits bits (128 KiB) that a 1,024-thread block keeps in LDS;
+  // a lane reads its L2 filter word only where this bit is set (empty: not built)
+  std::vector<uint32_t> h_bpf;
+  int32_t bs_pf_log2 = 20;        // its size: 2^bs_pf_log2 bits (kBsPfLog2Bits unless CVD_BS_PF_LOG2)
   bool rtc_bs = false;            // the specialised kernel built for this model is k1s
   int32_t slot0 = 0;              // row of D_0 = 0 (always 0)
   std::vector<uint32_t> bmp;      // [2^n/2][2^m][2^k] packed (bm(q0), bm(q1)) branch metrics
@@ -74,6 +79,7 @@ struct cvd_model {
   void* rtc_fn_multi = nullptr;    // its multi-model entry (cvd_detect_multi), same module
   int rtc_block = 256;             // its block size (1,024 with the LDS-resident filter)
   bool rtc_ldsf = false;           // it reads the Bloom filter from dynamic LDS (fcap * 4 bytes)
+  bool rtc_pf = false;             // it tests the LDS pre-filter h_bpf before the L2 filter (k1s)
   std::string jit_error;           // why the specialised kernel is unavailable (empty if built or n/a)
   std::vector<uint32_t> bfly;      // [2^m / 2]
 
@@ -93,6 +99,7 @@ struct cvd_model {
   uint32_t* d_bfilt_lds = nullptr;
   uint32_t* d_bkey = nullptr;
   uint32_t* d_bdkey = nullptr;
+  uint32_t* d_bpf = nullptr;
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
   uint32_t* d_bfly = nullptr;
@@ -131,6 +138,9 @@ constexpr int64_t kLdsFilterMaxRows = 32768;
 // the LDS filter's size (2^log2 words) and row cap: kLdsFilterLog2 / kLdsFilterMaxRows unless
 // CVD_LDSF_LOG2 (13..15; 15: 128 KiB, 1,024-thread blocks) / CVD_LDSF_MAX_ROWS set them
 int ldsf_log2();
+// the k1s LDS pre-filter (cvd_bitslice.h kBsPfLog2Bits: 128 KiB of dynamic LDS, 1,024-thread
+// blocks) for bit-sliced models without the LDS-resident filter, unless CVD_BS_PF=0
+bool bs_pf_preferred(const cvd_model& M, bool ldsf);
 int64_t ldsf_max_rows();
 bool ldsf_preferred(const cvd_model& M);
 int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,

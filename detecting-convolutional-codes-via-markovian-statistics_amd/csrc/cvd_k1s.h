@@ -31,6 +31,11 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #ifndef CVD_K1S_ABL
 #define CVD_K1S_ABL 0
 #endif
+// the LDS pre-filter variant (cvd_kernels.hip upload_model; 1,024-thread blocks, 128 KiB of
+// dynamic LDS): a lane tests D_t's pre-filter bit before it requests its L2 filter word
+#ifndef CVD_K1S_PF
+#define CVD_K1S_PF 0
+#endif
 
 // LDS: per (phase, y) two uint4 {e0, e1, ez, 0} of word 0 and word 1 (cvd::bs_eplanes)
 __device__ __forceinline__ uint4* bs_etab_lds() {
@@ -79,10 +84,13 @@ struct BsCursor {
   }
   // the two-step record (learned row s, words rn then rnn): {log P̂1 of both steps, row after
   // one step + 1, row after two + 1} (cvd_host.cpp, t2)
+  // (every k1s offset is a 32-bit byte offset from the table's base: the host keeps the
+  // bit-sliced tables under 4 GiB)
   __device__ void prefetch_t2(const ExpArgs& a, int32_t s, uint32_t rn, uint32_t rnn) {
-    const uint32_t* e = a.t2 + ((size_t)s * 16u + (rn | (rnn << 2))) * 8u;
-    const uint4 v = *reinterpret_cast<const uint4*>(e);
-    const uint2 w = *reinterpret_cast<const uint2*>(e + 4);
+    uint32_t o;
+    asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(o) : "v"(rn | (rnn << 2)), "v"((uint32_t)s << 9));
+    const uint4 v = ld_off<uint4>(a.t2, o);
+    const uint2 w = ld_off<uint2>(a.t2, o + 16u);
     plp = __hiloint2double((int)v.y, (int)v.x);
     plp2 = __hiloint2double((int)v.w, (int)v.z);
     pnx = (int32_t)(w.x & 0x0FFFFFFFu) - 1;
@@ -107,11 +115,9 @@ struct BsCursor {
 #pragma unroll
     for (int w = 0; w < 8; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
   }
-  __device__ static const uint32_t* slot_ptr(const ExpArgs& a, uint32_t s) {
-    return a.hkey + ((size_t)s << kBsSlotShift);
-  }
-  __device__ static void load_image(const uint32_t* p, uint32_t (&k)[8]) {
-    const uint4 u = *reinterpret_cast<const uint4*>(p), v = *reinterpret_cast<const uint4*>(p + 4);
+  __device__ static uint32_t slot_off(uint32_t s) { return s << (kBsSlotShift + 2); }
+  __device__ static void load_image(const uint32_t* base, uint32_t o, uint32_t (&k)[8]) {
+    const uint4 u = ld_off<uint4>(base, o), v = ld_off<uint4>(base, o + 16u);
     k[0] = u.x; k[1] = u.y; k[2] = u.z; k[3] = u.w; k[4] = v.x; k[5] = v.y; k[6] = v.z; k[7] = v.w;
   }
   // filter positive: the home slot's image of phase PH and its record for word r
@@ -119,9 +125,9 @@ struct BsCursor {
   __device__ void mid(const ExpArgs& a, uint32_t r) {
     cand = slot == -2 && ((fb & ~fw) | (fb1 & ~fw1)) == 0u;
     if (cand) {
-      const uint32_t* sp = slot_ptr(a, hs);
-      load_image(sp + 8 * PH, pkey);
-      const uint4 v = *reinterpret_cast<const uint4*>(sp + kBsRecWord + 4u * r);
+      const uint32_t so = slot_off(hs);
+      load_image(a.hkey, so + 32u * PH, pkey);
+      const uint4 v = ld_off<uint4>(a.hkey, so + 4u * kBsRecWord + 16u * r);
       pc = v.w;
       pnx = (int32_t)v.z;
       plp = __hiloint2double((int)v.y, (int)v.x);
@@ -156,11 +162,11 @@ struct BsCursor {
         uint32_t sl = hs;
         for (int pr = 1; pr <= a.max_probe; ++pr) {
           sl = (sl + 1u) & a.hmask;
-          const uint32_t* sp = slot_ptr(a, sl);
-          const uint4 v = *reinterpret_cast<const uint4*>(sp + kBsRecWord + 4u * r);
+          const uint32_t so = slot_off(sl);
+          const uint4 v = ld_off<uint4>(a.hkey, so + 4u * kBsRecWord + 16u * r);
           if (v.w == 0u) break;
           uint32_t k[8];
-          load_image(sp + 8 * PH, k);
+          load_image(a.hkey, so + 32u * PH, k);
           if (same(k, R)) {
             lpv = __hiloint2double((int)v.y, (int)v.x);
             ns = (int32_t)v.z;
@@ -196,7 +202,18 @@ struct BsCursor {
                                                        (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 3)));
       fb = pp.x;
       fb1 = pp.y;
-      const uint32_t fo = slot < 0 && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & a.fmask4) : 0u;
+#if CVD_K1S_PF
+      // the pre-filter bit of D_t (LDS): clear -- D_t is not a row -- and the lane reads filter
+      // word 0 like a lane that needs no lookup, with an all-ones pattern that word 0 cannot
+      // match (a match would only cost a wasted candidate test: the compare is exact)
+      const uint32_t pfw = *reinterpret_cast<const uint32_t*>(
+          reinterpret_cast<const char*>(dyn_lds()) + ((pl >> (32 - cvd::kBsPfLog2Bits + 5 - 2)) & ~3u));
+      const bool pos = ((pfw >> ((pl >> (32 - cvd::kBsPfLog2Bits)) & 31u)) & 1u) != 0u;
+      if (!pos) { fb = ~0u; fb1 = ~0u; }
+#else
+      constexpr bool pos = true;
+#endif
+      const uint32_t fo = slot < 0 && pos && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & a.fmask4) : 0u;
 #if CVD_K1B_LDSF
       const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + fo);
 #else
@@ -269,9 +286,10 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   auto walk_prefetch = [&]() {
     const uint32_t x = __builtin_amdgcn_alignbit(nxtw, curw, 2u * (pos & 15u));   // r of steps pos + 1, pos + 2
     if (two_steps()) {
-      const uint32_t* e = a.t2 + ((size_t)cur.slot * 16u + (x & 15u)) * 8u;
-      const uint4 v = *reinterpret_cast<const uint4*>(e);
-      const uint2 w = *reinterpret_cast<const uint2*>(e + 4);
+      uint32_t o;
+      asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(o) : "v"(x & 15u), "v"((uint32_t)cur.slot << 9));
+      const uint4 v = ld_off<uint4>(a.t2, o);
+      const uint2 w = ld_off<uint2>(a.t2, o + 16u);
       cur.pc = w.y;
       cur.pnx = (int32_t)w.x;
       plp2 = __hiloint2double((int)v.w, (int)v.z);
@@ -338,8 +356,8 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
           auto leave = [&]() {
             mode = kWalkAcs;
             cur.pnx = -1;
-            const uint32_t* kp = a.dkey + (size_t)cur.slot * kBsDkeyWords + 8u * phw;
-            const uint4 u = *reinterpret_cast<const uint4*>(kp), v = *reinterpret_cast<const uint4*>(kp + 4);
+            const uint32_t ko = (uint32_t)cur.slot * (4u * kBsDkeyWords) + 32u * phw;
+            const uint4 u = ld_off<uint4>(a.dkey, ko), v = ld_off<uint4>(a.dkey, ko + 16u);
             R[0][0] = u.x; R[0][1] = u.y; R[0][2] = u.z; R[0][3] = u.w;
             R[1][0] = v.x; R[1][1] = v.y; R[1][2] = v.z; R[1][3] = v.w;
           };
@@ -426,6 +444,12 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
     uint4* d = reinterpret_cast<uint4*>(dyn_lds());
     const uint4* g = reinterpret_cast<const uint4*>(a.filt);
     for (uint32_t i = threadIdx.x; i < (a.fmask + 1u) / 2u; i += blockDim.x) d[i] = g[i];
+  }
+#elif CVD_K1S_PF
+  {   // the pre-filter, 2^kBsPfLog2Bits bits, into dynamic LDS
+    uint4* d = reinterpret_cast<uint4*>(dyn_lds());
+    const uint4* g = reinterpret_cast<const uint4*>(a.pf);
+    for (uint32_t i = threadIdx.x; i < (1u << (cvd::kBsPfLog2Bits - 7)); i += blockDim.x) d[i] = g[i];
   }
 #endif
   __syncthreads();

@@ -1705,6 +1705,13 @@ bool cvd::walk_preferred(const cvd_model& M, bool early) {
   return !early && M.kind == 1 && M.learn_len_eff > 0 && 10 * M.n_rows < M.learn_len_eff;
 }
 
+// dynamic LDS of the specialised kernel: the LDS-resident filter or the k1s pre-filter
+static unsigned rtc_dyn_lds(const cvd_model& M) {
+  if (M.rtc_ldsf) return (unsigned)(M.fcap * sizeof(uint32_t));
+  if (M.rtc_pf) return (unsigned)(M.h_bpf.size() * sizeof(uint32_t));
+  return 0u;
+}
+
 // The explicit path's launch arguments of one model over one stream buffer.
 static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int64_t N, int64_t nseq, int64_t n_h1,
                         double* d_sums, int64_t* d_counts, uint8_t* d_trace, const uint32_t* bmp, bool early) {
@@ -1731,6 +1738,7 @@ static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int6
   a.early = early && !d_sums && !d_trace; a.lt_min = M.ltref[1]; a.lp_min = M.lp_min;
   a.dkey = bs ? M.d_bdkey : M.d_dkey;
   a.err = M.d_err;
+  a.pf = bs && M.rtc_pf ? M.d_bpf : nullptr;
   a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
@@ -1761,7 +1769,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   if (which == CVD_KERNEL_BUTTERFLY_RTC) {
     void* args[] = {&a};
     const unsigned blk = (unsigned)M.rtc_block, rgrid = (unsigned)((nseq + blk - 1) / blk);
-    const unsigned lds = M.rtc_ldsf ? (unsigned)(M.fcap * sizeof(uint32_t)) : 0u;   // the filter (CVD_K1B_LDSF)
+    const unsigned lds = rtc_dyn_lds(M);   // the filter (CVD_K1B_LDSF) or the pre-filter (CVD_K1S_PF)
     HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M.rtc_fn, rgrid, 1, 1, blk, 1, 1, lds,
                                     (hipStream_t)stream, args, nullptr));
     return CVD_OK;
@@ -1795,7 +1803,7 @@ static int launch_multi(const cvd_model* const* models, int32_t i0, int32_t i1, 
   if (ma.nm == 0) return CVD_OK;
   for (int j = ma.nm; j < kMultiMax; ++j) ma.blk_end[j] = blocks;
   void* args[] = {&ma};
-  const unsigned lds = M0.rtc_ldsf ? (unsigned)(M0.fcap * sizeof(uint32_t)) : 0u;
+  const unsigned lds = rtc_dyn_lds(M0);
   HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M0.rtc_fn_multi, blocks, 1, 1, blk, 1, 1, lds, (hipStream_t)stream,
                                   args, nullptr));
   return CVD_OK;
@@ -1830,6 +1838,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_bfilt_lds, M.h_bfilt_lds))) return rc;
     if ((rc = dev_copy(M.d_bkey, M.h_bkey))) return rc;
     if ((rc = dev_copy(M.d_bdkey, M.h_bdkey))) return rc;
+    if ((rc = dev_copy(M.d_bpf, M.h_bpf))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
     if ((rc = dev_copy(M.d_bmk1, M.bmk1))) return rc;
     if ((rc = dev_copy(M.d_bfly, M.bfly))) return rc;
@@ -1848,22 +1857,27 @@ int cvd::upload_model(cvd_model& M, int device) {
   M.rtc_fn_multi = nullptr;
   M.jit_error.clear();
   M.rtc_ldsf = M.k1b_ok && M.hcap > 0 && ldsf_preferred(M);
-  // block size: 512 threads with the LDS filter (two blocks of 8 waves per CU hold it),
-  // else 256 (CVD_K1B_BLOCK=256/512/1024 overrides, timing studies)
-  M.rtc_block = env_i("CVD_K1B_BLOCK", M.rtc_ldsf ? (M.fcap > ((int64_t)1 << 14) ? 1024 : 512) : kBlock);
-  if (M.rtc_block != 256 && M.rtc_block != 512 && M.rtc_block != 1024) M.rtc_block = kBlock;
-  // the bit-sliced form (k1s) for models with the bit-sliced tables; if it cannot be
-  // built, the butterfly kernel on the nibble tables
+  // the bit-sliced form (k1s) for models with the bit-sliced tables, with the LDS pre-filter
+  // where the model has one; if it cannot be built, the butterfly kernel on the nibble tables
   M.rtc_bs = false;
+  M.rtc_pf = false;
   for (int attempt = M.bs && M.d_bkey ? 0 : 1; attempt < 2 && M.k1b_ok && M.hcap > 0; ++attempt) {
     const bool bs = attempt == 0;
+    const bool pf = bs && !M.rtc_ldsf && M.d_bpf != nullptr;
+    // block size: 512 threads with the LDS filter (two blocks of 8 waves per CU hold it),
+    // 1,024 with the 128-KiB LDS filter or the pre-filter (one block per CU), else 256
+    // (CVD_K1B_BLOCK=256/512/1024 overrides the first and last, timing studies)
+    M.rtc_block = pf ? (M.bs_pf_log2 >= 20 ? 1024 : 512) : env_i("CVD_K1B_BLOCK", M.rtc_ldsf ? (M.fcap > ((int64_t)1 << 14) ? 1024 : 512) : kBlock);
+    if (M.rtc_block != 256 && M.rtc_block != 512 && M.rtc_block != 1024) M.rtc_block = kBlock;
     const int patbits = M.rtc_ldsf ? kFilterPatBitsLds : bs ? M.bs_pat_bits : kFilterPatBits;
     const std::string vdefs = "-DCVD_K1B_BLOCK=" + std::to_string(M.rtc_block) +
                               (M.rtc_ldsf ? " -DCVD_K1B_LDSF=1" : "") +
                               (patbits != kFilterPatBits ? " -DCVD_FILTER_PAT_BITS=" + std::to_string(patbits) : "") +
-                              (bs ? " -DCVD_K1B_BITSLICE=1" : "");
+                              (bs ? " -DCVD_K1B_BITSLICE=1" : "") + (pf ? " -DCVD_K1S_PF=1" : "") +
+                              (pf && M.bs_pf_log2 != kBsPfLog2Bits ? " -DCVD_K1S_PF_LOG2=" + std::to_string(M.bs_pf_log2) : "");
     if (rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn, &M.rtc_fn_multi) == 0) {
       M.rtc_bs = bs;
+      M.rtc_pf = pf;
       M.jit_error.clear();
       break;
     }
@@ -1884,13 +1898,14 @@ void cvd::free_model_device(cvd_model& M) {
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
   void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_filt_lds, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
-                  M.d_bmk1, M.d_bfly, M.d_err, M.d_bfilt, M.d_bfilt_lds, M.d_bkey, M.d_bdkey};
+                  M.d_bmk1, M.d_bfly, M.d_err, M.d_bfilt, M.d_bfilt_lds, M.d_bkey, M.d_bdkey, M.d_bpf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
   M.d_filt = nullptr; M.d_filt_lds = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_t2 = nullptr;
-  M.d_bfilt = nullptr; M.d_bfilt_lds = nullptr; M.d_bkey = nullptr; M.d_bdkey = nullptr;
+  M.d_bfilt = nullptr; M.d_bfilt_lds = nullptr; M.d_bkey = nullptr; M.d_bdkey = nullptr; M.d_bpf = nullptr;
   M.rtc_bs = false;
+  M.rtc_pf = false;
   M.d_bmp = nullptr;
   M.d_bmk1 = nullptr;
   M.d_bfly = nullptr;
@@ -1976,7 +1991,7 @@ static bool multi_ok(const cvd_model& M) {
 }
 static bool multi_same(const cvd_model& A, const cvd_model& B) {
   return A.rtc_fn_multi == B.rtc_fn_multi && A.rtc_block == B.rtc_block && A.rtc_ldsf == B.rtc_ldsf &&
-         A.rtc_bs == B.rtc_bs && (!A.rtc_bs || A.bs_pat_bits == B.bs_pat_bits) && A.device == B.device &&
+         A.rtc_bs == B.rtc_bs && A.rtc_pf == B.rtc_pf && (!A.rtc_pf || A.bs_pf_log2 == B.bs_pf_log2) && (!A.rtc_bs || A.bs_pat_bits == B.bs_pat_bits) && A.device == B.device &&
          (!A.rtc_ldsf || A.fcap == B.fcap);
 }
 // the same criterion as one id (cvd_model_info.multi_variant: the Python host groups launches
@@ -1986,7 +2001,7 @@ int64_t cvd::multi_variant(const cvd_model& M) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
   mix((uint64_t)(uintptr_t)M.rtc_fn_multi); mix((uint64_t)M.rtc_block); mix(M.rtc_ldsf ? 1u : 0u);
-  mix(M.rtc_bs ? 1u : 0u); mix((uint64_t)(M.device + 1)); mix(M.rtc_ldsf ? (uint64_t)M.fcap : 0u);
+  mix(M.rtc_bs ? 1u : 0u); mix(M.rtc_pf ? (uint64_t)M.bs_pf_log2 : 0u); mix((uint64_t)(M.device + 1)); mix(M.rtc_ldsf ? (uint64_t)M.fcap : 0u);
   return (int64_t)(h | 1u);
 }
 

@@ -93,6 +93,15 @@ CVD_HD void key_hash_less(const unsigned* w, int nw, unsigned c, unsigned& ph, u
 #endif
 constexpr int kFilterPatBits = CVD_FILTER_PAT_BITS, kFilterPatterns = 1 << kFilterPatBits;
 constexpr int kFilterPatBitsLds = 10;
+// The bit-sliced kernel's LDS pre-filter (cvd_k1s.h, CVD_K1S_PF): one bit per row at index
+// pl >> (32 - kBsPfLog2Bits) of its key hash, 2^20 bits = 128 KiB, one copy per 1,024-thread
+// block (one block per CU, beside the 1,024-pair pattern table); a lane whose bit is clear
+// skips its L2 filter read (built by cvd_host.cpp build_hash)
+// (CVD_K1S_PF_LOG2=19: 64 KiB in 512-thread blocks, two per CU; timing studies)
+#ifndef CVD_K1S_PF_LOG2
+#define CVD_K1S_PF_LOG2 20
+#endif
+constexpr int kBsPfLog2Bits = CVD_K1S_PF_LOG2;
 CVD_HD unsigned filter_pattern(unsigned i) {
   unsigned x = (i + 1u) * 0x9E3779B1u;
   x ^= x >> 15;

@@ -241,7 +241,7 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
     std::string t;
     while (ds >> t)
       if (t.rfind("-DCVD_K1B_BLOCK", 0) != 0 && t.rfind("-DCVD_K1B_LDSF", 0) != 0 &&
-          t.rfind("-DCVD_FILTER_PAT_BITS", 0) != 0)
+          t.rfind("-DCVD_FILTER_PAT_BITS", 0) != 0 && t.rfind("-DCVD_K1S_PF", 0) != 0)
         env_defs += " " + t;
   }
   const std::string all_defs = std::string(variant_defs ? variant_defs : "") + env_defs;

@@ -43,9 +43,9 @@ def main():
         src = os.path.join(d, "k1b_spec.hip")
         with open(src, "w") as f:
             f.write('#include <hip/hip_runtime.h>\n#include "cvd_device.h"\n'
-                    'extern "C" __global__ __launch_bounds__(cvd_dev::kBlock, cvd_dev::kK1bWavesPerSimd)\n'
+                    'extern "C" __global__ __launch_bounds__(cvd_dev::kK1bBlock, cvd_dev::kK1bWavesPerSimd)\n'
                     f'void cvd_k1b_spec(cvd_dev::ExpArgs a) {{ cvd_dev::k1b_spec_entry<{m}, 0x{xm:016x}ull>(a); }}\n'
-                    'extern "C" __global__ __launch_bounds__(cvd_dev::kBlock, cvd_dev::kK1bWavesPerSimd)\n'
+                    'extern "C" __global__ __launch_bounds__(cvd_dev::kK1bBlock, cvd_dev::kK1bWavesPerSimd)\n'
                     f'void cvd_k1b_spec_multi(cvd_dev::MultiArgs a) {{ cvd_dev::k1b_spec_multi_entry<{m}, 0x{xm:016x}ull>(a); }}\n')
         base = [clang, "-x", "hip", "--offload-arch=gfx950", "--offload-device-only", "--no-gpu-bundle-output",
                 "-O3", "-std=c++17", "-ffp-contract=off", "-mllvm", "--amdgpu-sched-strategy=max-ilp",
