@@ -810,38 +810,52 @@ __global__ __launch_bounds__(kBlock) void detect_table_kernel(TabArgs a) {
 // The only dependent chain is the u16 record (next state).  The received words are
 // read in 16-byte chunks one chunk ahead (64 or 40 steps of lead), and full chunks run
 // fully unrolled.
-template <int n, bool kLr>
+//  * kCp > 1 (kLr only; timing studies, CVD_C1_COPIES): kCp interleaved copies of the
+//    kLr image, entry i of copy c at element i kCp + c, lane l reading copy l mod kCp, so
+//    lanes of one LDS lane group that gather different entries fall on different banks
+//    more often; records hold next * 2^n * kCp.
+//  * kLpG (kLr = false only; timing studies, CVD_T16_LPG=1): the 16-bit records and log
+//    T_ref(c) in LDS, log P̂1 gathered from global memory (L1/L2) -- 2 B per entry of LDS
+//    instead of 10.
+typedef const __attribute__((address_space(1))) double gdouble;
+template <int n, bool kLr, int kCp = 1, bool kLpG = false>
 struct LdsModel {
+  static_assert(kCp == 1 || kLr, "copies of the kLr image only");
+  static_assert(!(kLpG && kLr), "log P̂1 from global memory with the 10-B image only");
   static constexpr uint32_t R = 1u << n;
   const double* lp;      // [SR] log P̂1
+  gdouble* lpg;          // kLpG: [SR] log P̂1 in global memory
   const double* lt;      // kLr: [SR] log T_ref(i, r); else [R + 1] log(c / 2^n)
   const uint16_t* rec;   // kLr: [SR] next * 2^n; else [SR] next << 4 | c
   __host__ __device__ static size_t bytes(int64_t SR) {
-    return kLr ? (size_t)SR * 18 : (size_t)SR * 10 + (R + 1) * sizeof(double);
+    return kLr ? (size_t)SR * 18 * kCp : (size_t)SR * (kLpG ? 2 : 10) + (R + 1) * sizeof(double);
   }
   __device__ void fill(const TabArgs& a, char* smem, int BS) {
     const int SR = (int)a.S * (int)R;
     double* s_lp = reinterpret_cast<double*>(smem);
-    double* s_lt = s_lp + SR;
-    uint16_t* s_rec = reinterpret_cast<uint16_t*>(s_lt + (kLr ? SR : (int)R + 1));
-    for (int i = threadIdx.x; i < SR; i += BS) {
+    double* s_lt = s_lp + (kLpG ? 0 : SR * kCp);
+    uint16_t* s_rec = reinterpret_cast<uint16_t*>(s_lt + (kLr ? SR * kCp : (int)R + 1));
+    lpg = (gdouble*)a.logp1;
+    for (int j = threadIdx.x; j < SR * kCp; j += BS) {
+      const int i = j / kCp;
       const uint32_t e = a.rec[i];
-      s_lp[i] = a.logp1[i];
+      if constexpr (!kLpG) s_lp[j] = a.logp1[i];
       if constexpr (kLr) {
-        s_lt[i] = a.ltref[e & 15u];
-        s_rec[i] = (uint16_t)((e >> 4) * R);   // S * 2^n < 65536 (host-checked)
+        s_lt[j] = a.ltref[e & 15u];
+        s_rec[j] = (uint16_t)((e >> 4) * R * kCp);   // S * 2^n * kCp < 65536 (host-checked)
       } else {
-        s_rec[i] = (uint16_t)e;                // next < 4096: next << 4 | c fits 16 bits (host-checked)
+        s_rec[j] = (uint16_t)e;                // next < 4096: next << 4 | c fits 16 bits (host-checked)
       }
     }
     if constexpr (!kLr)
       for (int i = threadIdx.x; i <= (int)R; i += BS) s_lt[i] = a.ltref[i];
-    lp = s_lp; lt = s_lt; rec = s_rec;
+    const uint32_t c = kCp > 1 ? (threadIdx.x & (uint32_t)(kCp - 1)) : 0u;
+    lp = s_lp + c; lt = s_lt + c; rec = s_rec + c;
   }
   // st: the state's entry base (kLr) or index; state 0 is 0 either way
   __device__ __forceinline__ void step(uint32_t& st, uint32_t r, double& lps, double& lrs) const {
     if constexpr (kLr) {
-      const uint32_t idx = st + r;
+      const uint32_t idx = st + r * (uint32_t)kCp;
       const uint32_t nx = rec[idx];
       lps += lp[idx];                 // log P̂1[i, j]   (Pd_plotter.py:213)
       lrs += lt[idx];                 // log T_ref[i, j] (Pd_plotter.py:214)
@@ -849,7 +863,7 @@ struct LdsModel {
     } else {
       const uint32_t idx = st * R + r;
       const uint32_t e = rec[idx];
-      lps += lp[idx];                 // log P̂1[i, j]   (Pd_plotter.py:213)
+      lps += kLpG ? lpg[idx] : lp[idx];   // log P̂1[i, j]   (Pd_plotter.py:213)
       lrs += lt[e & 15u];             // log T_ref[i, j] = log(c / 2^n) (Pd_plotter.py:214)
       st = e >> 4;
     }
@@ -860,11 +874,11 @@ struct LdsModel {
   }
 };
 
-template <int n, int BS, bool kLr>
+template <int n, int BS, bool kLr, bool kLpG = false>
 __global__ __launch_bounds__(BS) void detect_table16_kernel(TabArgs a) {
   constexpr int SPW = 32 / n;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  LdsModel<n, kLr> md;
+  LdsModel<n, kLr, 1, kLpG> md;
   md.fill(a, smem, BS);
   __syncthreads();
   const int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x;
@@ -928,15 +942,15 @@ struct FusedArgs {
   int64_t trial_begin, T, Tp;
 };
 
-template <int k, int n, int BS, bool kLr, int kT = 0>
+template <int k, int n, int BS, bool kLr, int kT = 0, int kCp = 1>
 __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
   constexpr int SPW = 32 / n;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const TabArgs& ta = a.t;
-  LdsModel<n, kLr> md;
+  LdsModel<n, kLr, kCp> md;
   md.fill(ta, smem, BS);
   // the noise exchange's slot records, 2 x 64 words per wave, after the model
-  uint32_t* s_x = reinterpret_cast<uint32_t*>(smem + ((LdsModel<n, kLr>::bytes(ta.S * (1 << n)) + 15) & ~(size_t)15));
+  uint32_t* s_x = reinterpret_cast<uint32_t*>(smem + ((LdsModel<n, kLr, kCp>::bytes(ta.S * (1 << n)) + 15) & ~(size_t)15));
   __syncthreads();
   uint32_t* su = s_x + (threadIdx.x / 64) * 128;
   uint32_t* sm = su + 64;
@@ -1538,6 +1552,11 @@ bool table_lr(const cvd_model& M) {
 }
 }  // namespace
 
+static int env_i(const char* name, int def) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atoi(e) : def;
+}
+
 int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int64_t nseq,
                              int64_t n_h1, double* d_sums, int64_t* d_counts, void* stream, bool early) {
   if (M.kind != 0 || !M.d_rec) { set_error("table path needs a dense (enumerated) model"); return CVD_E_UNSUPPORTED; }
@@ -1559,12 +1578,19 @@ int cvd::launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N,
     // log T_ref gathers spread over S 2^n entries instead of 2^n + 1 broadcast ones --
     // m2 overlapped step 43.6 -> 47.2 ms, profiles/r03f/; the fused kernel, VALU-bound,
     // gains from it)
-    const size_t lds = lds16;
+    size_t lds = lds16;
     void (*kern)(TabArgs) = M.dec.n == 2 ? (big ? detect_table16_kernel<2, 1024, false> : detect_table16_kernel<2, kBlock, false>)
                                          : (big ? detect_table16_kernel<3, 1024, false> : detect_table16_kernel<3, kBlock, false>);
+    int bsl = bs;
+    // (timing studies: the records in LDS and log P̂1 from global memory, 256-thread blocks)
+    if (M.dec.n == 3 && env_i("CVD_T16_LPG", 0) == 1) {
+      kern = detect_table16_kernel<3, kBlock, false, true>;
+      lds = LdsModel<3, false, 1, true>::bytes((int64_t)M.S * R);
+      bsl = kBlock;
+    }
     if (lds > 64 * 1024)
       HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(kern, dim3((unsigned)((nseq + bs - 1) / bs)), dim3(bs), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((nseq + bsl - 1) / bsl)), dim3(bsl), lds, (hipStream_t)stream, a);
     HIP_CHECK(hipGetLastError());
     return CVD_OK;
   }
@@ -1600,7 +1626,14 @@ int cvd::launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc&
   const bool big = lds16 > 40 * 1024;
   const int bs = big ? 1024 : kBlock;
   const bool lr = !big && table_lr(M);
-  const size_t limg = lr ? (size_t)M.S * R * 18 : lds16;
+  // interleaved copies of the small image (timing studies, LdsModel kCp): CVD_C1_COPIES =
+  // 4, 8 or 16 for rate-1/2 codes of at most 3 taps per output
+  const int kt0 = tap_slots(std::max(gen_args(e1, k0, k1, tag, thr, N, 1).ntap, gen_args(e2, k0, k1, tag, thr, N, 1).ntap));
+  int cp = env_i("CVD_C1_COPIES", 1);
+  if (!(lr && M.dec.k == 1 && M.dec.n == 2 && kt0 == 3 && (cp == 4 || cp == 8 || cp == 16) &&
+        (int64_t)M.S * R * cp < 65536))
+    cp = 1;
+  const size_t limg = lr ? (size_t)M.S * R * 18 * cp : lds16;
   const size_t lds = ((limg + 15) & ~(size_t)15) + (size_t)(bs / 64) * 128 * sizeof(uint32_t);
   const int k = M.dec.k, n = M.dec.n;
   if (M.kind != 0 || !M.d_rec || M.S >= 4096 || lds > 160 * 1024 || std::getenv("CVD_MC_UNFUSED") ||
@@ -1621,7 +1654,10 @@ int cvd::launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc&
   void (*kern)(FusedArgs) = nullptr;
   // unrolled tap lists for rate 1/2 (C1) with at most 3 or 5 taps per output
   const int kt = tap_slots(std::max(a.g[0].ntap, a.g[1].ntap));
-  if (k == 1 && n == 2 && kt == 3)
+  if (k == 1 && n == 2 && kt == 3 && cp > 1)
+    kern = cp == 4 ? mc_table16_kernel<1, 2, kBlock, true, 3, 4> : cp == 8 ? mc_table16_kernel<1, 2, kBlock, true, 3, 8>
+                                                                  : mc_table16_kernel<1, 2, kBlock, true, 3, 16>;
+  else if (k == 1 && n == 2 && kt == 3)
     kern = big ? mc_table16_kernel<1, 2, 1024, false, 3> : lr ? mc_table16_kernel<1, 2, kBlock, true, 3>
                                                             : mc_table16_kernel<1, 2, kBlock, false, 3>;
   else if (k == 1 && n == 2 && (kt == 4 || kt == 5))
@@ -1667,11 +1703,6 @@ int cvd::explicit_kernel_of(const cvd_model& M) {
   const uint32_t* b;
   const int which = select_explicit(M, kExplicitBest, &k, &b);
   return which == CVD_KERNEL_BUTTERFLY_RTC && M.rtc_bs ? CVD_KERNEL_BITSLICE_RTC : which;
-}
-
-static int env_i(const char* name, int def) {
-  const char* e = std::getenv(name);
-  return e && *e ? std::atoi(e) : def;
 }
 
 // k1b_walk (cvd_device.h) for the H1 waves of the specialised kernel.  Its walks pay
