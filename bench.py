@@ -560,7 +560,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u16x2 (metrics) + f64 (log-likelihood sums)",
+        "dtype": ("u32 bit-planes (metrics, four planes of the 64 states) + f64 (log-likelihood sums)"
+                  if info.get("explicit_kernel") == 5 else "u16x2 (metrics) + f64 (log-likelihood sums)"),
         "data": "synthetic: Philox4x32-10 encoder inputs and BSC(p) flips (build spec), learned P̂1",
         "config": {"name": a.config, "detector": a.detector,
                    "workload": (f"{a.config} pair {cc['gen1']} vs {cc['gen2']}, N={N}, p-sweep {p_grid}, "
@@ -617,6 +618,8 @@ def main():
         out["cpu_baseline"], _ = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds, host)
         out["pd_match_vs_cpu"] = pd_match(pkg, det, cc, a.config, k, n, m, a.seed, a.cpu_seconds, host)
         out["c0_demo"] = c0_demo(pkg, host)
+        if a.config == "m6":
+            out["reference_call"] = reference_call(pkg, cc, k, n, m, N, p_grid, a.learn_len, a.seed)
     print(json.dumps(out, default=_json_default), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -750,7 +753,8 @@ def run_c4(a, pkg, world, rank, local, dist):
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u16x2 (metrics) + f64 (log-likelihood sums)",
+        "dtype": ("u32 bit-planes (metrics, four planes of the 64 states) + f64 (log-likelihood sums)"
+                  if info.get("explicit_kernel") == 5 else "u16x2 (metrics) + f64 (log-likelihood sums)"),
         "data": "synthetic: Philox4x32-10 encoder inputs and BSC(p) flips (build spec), learned P̂1",
         "config": {"name": "c4", "workload": f"m6 pair {cc['gen1']} vs {cc['gen2']}, N in {Ns} x p {p_grid}, "
                                              f"{T} trials per grid point ({total} total), one step = one grid point",
@@ -955,6 +959,30 @@ def c0_demo(pkg, host):
     return {"config": "demo preset (7,5) vs (5,7), m=2, N=1e3, 1e3 trials, p " + str(c["p_vec"]),
             "cpu_seconds": t_cpu, "cpu_trials_per_s": len(c["p_vec"]) * c["trials"] / t_cpu, "cpu_threads": threads,
             "gpu_seconds_incl_setup": t_gpu, "rows": rows_gpu, "match": bool(rows_gpu == rows_cpu)}
+
+
+def reference_call(pkg, cc, k, n, m, N, p_grid, learn_len, seed, num_iter=10_000):
+    """The headline workload at the reference's own call shape: run_experiment with its
+    default num_iter = 10,000 trials per p (Pd_plotter.py:176-235, 242-264) over the C2 p grid
+    at N, through the product's drop-in (cvd_mc_run_grid: per N, each p's batch and one
+    multi-model detector launch for the row).  The first call includes the
+    models' learning and table builds and the kernel JIT (setup); the second finds them cached
+    and times the trials alone; both run every step of every trial (early_decision=False) and
+    must give the same DataFrame."""
+    import torch
+    args = (k, n, m, cc["gen1"], cc["gen2"], num_iter, list(p_grid), learn_len, 200, 1.0, seed)
+    t0 = time.perf_counter()
+    df1 = pkg.run_experiment(*args, N_list=[N], early_decision=False)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    df2 = pkg.run_experiment(*args, N_list=[N], early_decision=False)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    trials = num_iter * len(p_grid)
+    return {"call": f"run_experiment(num_iter={num_iter}, p_vec={list(p_grid)}, N_list=[{N}], learn_len={learn_len})",
+            "trials": trials, "first_call_s_incl_setup": t1 - t0, "second_call_s": t2 - t1,
+            "trials_per_s_second_call": trials / (t2 - t1),
+            "dataframes_equal": bool(df1.equals(df2)), "rows": df2.to_dict(orient="records")}
 
 
 if __name__ == "__main__":
