@@ -176,6 +176,7 @@ struct ExpArgs {
   double lt_min, lp_min;    // smallest log T_ref / log P̂1 increments (early_decide)
   int32_t* err;             // error flags (nullable): bit 0 = k1b_walk left its loop by the guard
   const uint32_t* pf;       // k1s LDS pre-filter (CVD_K1S_PF): 2^kBsPfLog2Bits bits, copied into dynamic LDS
+  uint32_t* wq;             // k1s persistent launch: work-queue counter (zeroed before the launch), else null
 };
 
 // Received words of one sequence, one word of lookahead (the next step's r is

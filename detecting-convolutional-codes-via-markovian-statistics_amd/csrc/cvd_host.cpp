@@ -679,10 +679,10 @@ void build_hash(cvd_model& Mo) {
   // (r1, r2), 32 B {log P̂1(d, r1), log P̂1(d1, r2), (d1 + 1) | c(d, r1) << 28,
   // (d2 + 1) | c(d1, r2) << 28}, d1 / d2 the rows after one / two steps (0 = not a row)
   Mo.h_t2.clear();
-  // (the bit-sliced kernel's lockstep lanes read them too: a lane walking learned rows loads
-  // one record per two steps; CVD_BS_T2=0 leaves them to the walking models)
+  // (CVD_BS_T2=1: for the bit-sliced lockstep lanes too, whose kernel reads them with
+  // -DCVD_K1S_T2=1 in CVD_JIT_DEFINES; timing studies, cvd_k1s.h)
   const char* bt2 = std::getenv("CVD_BS_T2");
-  if (Mo.dec.k == 1 && R == 4 && (walk_preferred(Mo) || (Mo.bs && !(bt2 && bt2[0] == '0')))) {
+  if (Mo.dec.k == 1 && R == 4 && (walk_preferred(Mo) || (Mo.bs && bt2 && bt2[0] == '1'))) {
     Mo.h_t2.assign((size_t)Mo.n_rows * 16 * 8, 0u);
     parallel_for(Mo.n_rows, [&](int64_t d, int) {
       const uint32_t* a0 = Mo.h_drow.data() + (size_t)d * Mo.h_rsw;

@@ -80,6 +80,7 @@ struct cvd_model {
   int rtc_block = 256;             // its block size (1,024 with the LDS-resident filter)
   bool rtc_ldsf = false;           // it reads the Bloom filter from dynamic LDS (fcap * 4 bytes)
   bool rtc_pf = false;             // it tests the LDS pre-filter h_bpf before the L2 filter (k1s)
+  int64_t rtc_persist_grid = 0;    // k1s: blocks of a persistent (work-queue) launch, 0 = none
   std::string jit_error;           // why the specialised kernel is unavailable (empty if built or n/a)
   std::vector<uint32_t> bfly;      // [2^m / 2]
 
@@ -100,6 +101,7 @@ struct cvd_model {
   uint32_t* d_bkey = nullptr;
   uint32_t* d_bdkey = nullptr;
   uint32_t* d_bpf = nullptr;
+  uint32_t* d_wq = nullptr;       // k1s persistent launches: kWqRing work-queue counters
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
   uint32_t* d_bfly = nullptr;

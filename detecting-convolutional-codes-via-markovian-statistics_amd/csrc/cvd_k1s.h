@@ -36,6 +36,14 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #ifndef CVD_K1S_PF
 #define CVD_K1S_PF 0
 #endif
+// two-step records for the lockstep lanes that walk learned rows (CVD_K1S_T2=1 with the
+// model's t2 table, CVD_BS_T2=1): one load per two steps.  Off by default: +1.5% at p = 0.05,
+// -0.8% to -2.6% at p >= 0.1 with the pre-filter (profiles/r05j: the 512-B-per-row table
+// spreads the walks over 8x the lines), and its 4 VGPRs
+#ifndef CVD_K1S_T2
+#define CVD_K1S_T2 0
+#endif
+constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
 
 // LDS: per (phase, y) two uint4 {e0, e1, ez, 0} of word 0 and word 1 (cvd::bs_eplanes)
 __device__ __forceinline__ uint4* bs_etab_lds() {
@@ -100,7 +108,7 @@ struct BsCursor {
   __device__ void start(const ExpArgs& a, uint32_t r0, uint32_t r1) {
     slot = a.slot0; hs = 0u; hsn = 0u; fb = 0u; fw = 0u; fb1 = 0u; fw1 = 0u; cand = false; pc = 1u; half = 0u;
     plp2 = 0.0; pnx2 = -1;
-    if (a.t2) prefetch_t2(a, slot, r0, r1);
+    if (kK1sT2 && a.t2) prefetch_t2(a, slot, r0, r1);
     else prefetch_row(a, slot, r0);
   }
   // ordering fences (RowCursor::fence): the waits for the loads issued a step / half a step
@@ -111,7 +119,8 @@ struct BsCursor {
     asm volatile("" : "+v"(fw), "+v"(fw1), "+v"(slot) : "v"(dep));
   }
   __device__ void fence_resolve(uint32_t dep) {
-    asm volatile("" : "+v"(slot), "+v"(pnx), "+v"(plp), "+v"(pc), "+v"(pnx2), "+v"(plp2) : "v"(dep));
+    asm volatile("" : "+v"(slot), "+v"(pnx), "+v"(plp), "+v"(pc) : "v"(dep));
+    if constexpr (kK1sT2) asm volatile("" : "+v"(pnx2), "+v"(plp2) : "v"(dep));
 #pragma unroll
     for (int w = 0; w < 8; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
   }
@@ -177,7 +186,7 @@ struct BsCursor {
     }
     slot = ns;
     // a two-step record's second step (its row after one step is D_t's): ready for the next
-    if (known && half == 1u && ns >= 0) {
+    if (kK1sT2 && known && half == 1u && ns >= 0) {
       plp = plp2; pnx = pnx2; half = 2u;
     } else {
       half = 0u;
@@ -228,8 +237,8 @@ struct BsCursor {
   // its own), and D_t's home slot becomes the pending lookup's
   template <bool kRow = true>
   __device__ void next(const ExpArgs& a, uint32_t rn, uint32_t rnn = 0u) {
-    if (kRow && slot >= 0 && half != 2u) {
-      if (a.t2) prefetch_t2(a, slot, rn, rnn);
+    if (kRow && slot >= 0 && (!kK1sT2 || half != 2u)) {
+      if (kK1sT2 && a.t2) prefetch_t2(a, slot, rn, rnn);
       else prefetch_row(a, slot, rn);
     }
     hs = hsn;
@@ -432,28 +441,10 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   count_decisions_masked(vmask, vmask, lp, lr, a.counts);
 }
 
+// one wave's 64 sequences [64 gw, 64 gw + 64) through the lockstep loop, or walk mode
 template <uint64_t XM>
-__device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
+__device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const double* s_lt) {
   constexpr bool kUni = xm_uni<6, XM>();
-  __shared__ double s_lt[5];
-  if (threadIdx.x <= 4) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
-  fill_filter_patterns();
-  fill_bs_etab<XM>();
-#if CVD_K1B_LDSF
-  {   // the whole filter, 2 (fmask + 1) words, into dynamic LDS
-    uint4* d = reinterpret_cast<uint4*>(dyn_lds());
-    const uint4* g = reinterpret_cast<const uint4*>(a.filt);
-    for (uint32_t i = threadIdx.x; i < (a.fmask + 1u) / 2u; i += blockDim.x) d[i] = g[i];
-  }
-#elif CVD_K1S_PF
-  {   // the pre-filter, 2^kBsPfLog2Bits bits, into dynamic LDS
-    uint4* d = reinterpret_cast<uint4*>(dyn_lds());
-    const uint4* g = reinterpret_cast<const uint4*>(a.pf);
-    for (uint32_t i = threadIdx.x; i < (1u << (cvd::kBsPfLog2Bits - 7)); i += blockDim.x) d[i] = g[i];
-  }
-#endif
-  __syncthreads();
-  int64_t gw = (int64_t)blk * (kK1bBlock / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
   if (a.walk) {
     // H1 and H2 waves alternate on every SIMD (k1b_body)
     const int64_t half = ((a.nseq + 63) / 64 + 1) / 2, k = gw >> 1;
@@ -551,6 +542,45 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
     early_final(dec, lp, lr);
   }
   count_decisions_masked(vmask, hmask, lp, lr, a.counts);
+}
+
+// The block's LDS tables, then its waves' sequences: by block index, or -- a.wq set, the
+// persistent launch of cvd_kernels.hip (one block per resident slot) -- from a work queue,
+// each wave taking the next 64 sequences until none are left, so that a CU's waves finish
+// together whatever their lookups cost and the LDS tables are filled once per block
+template <uint64_t XM>
+__device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
+  __shared__ double s_lt[5];
+  if (threadIdx.x <= 4) s_lt[threadIdx.x] = a.ltref[threadIdx.x];
+  fill_filter_patterns();
+  fill_bs_etab<XM>();
+#if CVD_K1B_LDSF
+  {   // the whole filter, 2 (fmask + 1) words, into dynamic LDS
+    uint4* d = reinterpret_cast<uint4*>(dyn_lds());
+    const uint4* g = reinterpret_cast<const uint4*>(a.filt);
+    for (uint32_t i = threadIdx.x; i < (a.fmask + 1u) / 2u; i += blockDim.x) d[i] = g[i];
+  }
+#elif CVD_K1S_PF
+  {   // the pre-filter, 2^kBsPfLog2Bits bits, into dynamic LDS
+    uint4* d = reinterpret_cast<uint4*>(dyn_lds());
+    const uint4* g = reinterpret_cast<const uint4*>(a.pf);
+    for (uint32_t i = threadIdx.x; i < (1u << (cvd::kBsPfLog2Bits - 7)); i += blockDim.x) d[i] = g[i];
+  }
+#endif
+  __syncthreads();
+  // every wave leaves once the queue is past the last unit (no block barrier below)
+  const uint32_t nunits = (uint32_t)((a.nseq + 63) / 64);   // < 2^32 (host: grid and queue limits)
+  auto take = [&]() -> uint32_t {
+    uint32_t u = 0u;
+    if (lane_id() == 0) u = atomicAdd(a.wq, 1u);
+    return __builtin_amdgcn_readfirstlane(u);
+  };
+  uint32_t u = a.wq ? take() : blk * (uint32_t)(kK1bBlock / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
+  while (u < nunits) {
+    k1s_wave<XM>(a, (int64_t)u, s_lt);
+    if (!a.wq) break;
+    u = take();
+  }
 }
 
 template <uint64_t XM>

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <string>
 
@@ -1736,6 +1737,8 @@ bool cvd::walk_preferred(const cvd_model& M, bool early) {
   return !early && M.kind == 1 && M.learn_len_eff > 0 && 10 * M.n_rows < M.learn_len_eff;
 }
 
+constexpr uint32_t kWqRing = 64;   // work-queue counters per model (persistent k1s launches)
+
 // dynamic LDS of the specialised kernel: the LDS-resident filter or the k1s pre-filter
 static unsigned rtc_dyn_lds(const cvd_model& M) {
   if (M.rtc_ldsf) return (unsigned)(M.fcap * sizeof(uint32_t));
@@ -1770,6 +1773,7 @@ static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int6
   a.dkey = bs ? M.d_bdkey : M.d_dkey;
   a.err = M.d_err;
   a.pf = bs && M.rtc_pf ? M.d_bpf : nullptr;
+  a.wq = nullptr;   // (launch_detect_explicit sets it for a persistent launch)
   a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
@@ -1799,8 +1803,18 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
   const unsigned grid = (unsigned)((nseq + kBlock - 1) / kBlock);
   if (which == CVD_KERNEL_BUTTERFLY_RTC) {
     void* args[] = {&a};
-    const unsigned blk = (unsigned)M.rtc_block, rgrid = (unsigned)((nseq + blk - 1) / blk);
+    const unsigned blk = (unsigned)M.rtc_block;
+    unsigned rgrid = (unsigned)((nseq + blk - 1) / blk);
     const unsigned lds = rtc_dyn_lds(M);   // the filter (CVD_K1B_LDSF) or the pre-filter (CVD_K1S_PF)
+    // k1s over more blocks than stay resident: one block per resident slot, the waves taking
+    // their sequences from a work queue (k1s_body); its counter, one of a ring per model, is
+    // zeroed on the launch's stream
+    if (M.rtc_bs && M.d_wq && M.rtc_persist_grid > 0 && (int64_t)rgrid > M.rtc_persist_grid) {
+      static std::atomic<uint32_t> seq{0};
+      a.wq = M.d_wq + (seq.fetch_add(1u) % kWqRing);
+      HIP_CHECK(hipMemsetAsync(a.wq, 0, sizeof(uint32_t), (hipStream_t)stream));
+      rgrid = (unsigned)M.rtc_persist_grid;
+    }
     HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M.rtc_fn, rgrid, 1, 1, blk, 1, 1, lds,
                                     (hipStream_t)stream, args, nullptr));
     return CVD_OK;
@@ -1920,6 +1934,18 @@ int cvd::upload_model(cvd_model& M, int device) {
     M.rtc_ldsf = false;
     M.rtc_block = kBlock;
   }
+  // persistent launches of k1s (CVD_K1S_PERSIST=0: one block per 64 x (block / 64) sequences):
+  // as many blocks as the device keeps resident
+  M.rtc_persist_grid = 0;
+  if (M.rtc_fn && M.rtc_bs && env_i("CVD_K1S_PERSIST", 1) != 0) {
+    int nb = 0, ncu = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (hipFunction_t)M.rtc_fn, M.rtc_block,
+                                                           rtc_dyn_lds(M)) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && nb > 0 && ncu > 0) {
+      HIP_CHECK(hipMalloc((void**)&M.d_wq, kWqRing * sizeof(uint32_t)));
+      M.rtc_persist_grid = (int64_t)nb * ncu;
+    }
+  }
   return CVD_OK;
 }
 
@@ -1929,12 +1955,13 @@ void cvd::free_model_device(cvd_model& M) {
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
   void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_filt_lds, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
-                  M.d_bmk1, M.d_bfly, M.d_err, M.d_bfilt, M.d_bfilt_lds, M.d_bkey, M.d_bdkey, M.d_bpf};
+                  M.d_bmk1, M.d_bfly, M.d_err, M.d_bfilt, M.d_bfilt_lds, M.d_bkey, M.d_bdkey, M.d_bpf, M.d_wq};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
   M.d_filt = nullptr; M.d_filt_lds = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_t2 = nullptr;
-  M.d_bfilt = nullptr; M.d_bfilt_lds = nullptr; M.d_bkey = nullptr; M.d_bdkey = nullptr; M.d_bpf = nullptr;
+  M.d_bfilt = nullptr; M.d_bfilt_lds = nullptr; M.d_bkey = nullptr; M.d_bdkey = nullptr; M.d_bpf = nullptr; M.d_wq = nullptr;
+  M.rtc_persist_grid = 0;
   M.rtc_bs = false;
   M.rtc_pf = false;
   M.d_bmp = nullptr;
