@@ -569,7 +569,10 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
 #endif
   __syncthreads();
   // every wave leaves once the queue is past the last unit (no block barrier below)
-  const uint32_t nunits = (uint32_t)((a.nseq + 63) / 64);   // < 2^32 (host: grid and queue limits)
+  // units: waves of 64 sequences; walk mode's H1 / H2 interleave (k1s_wave) permutes
+  // [0, 2 ceil(units / 2)), whose last unit may hold no sequence
+  uint32_t nunits = (uint32_t)((a.nseq + 63) / 64);   // < 2^32 (host: grid and queue limits)
+  if (a.walk) nunits = (nunits + 1u) & ~1u;
   auto take = [&]() -> uint32_t {
     uint32_t u = 0u;
     if (lane_id() == 0) u = atomicAdd(a.wq, 1u);

@@ -1809,11 +1809,14 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
     // k1s over more blocks than stay resident: one block per resident slot, the waves taking
     // their sequences from a work queue (k1s_body); its counter, one of a ring per model, is
     // zeroed on the launch's stream
-    if (M.rtc_bs && M.d_wq && M.rtc_persist_grid > 0 && (int64_t)rgrid > M.rtc_persist_grid) {
+    // (CVD_K1S_PERSIST=0: off; CVD_K1S_PERSIST_BLOCKS=b: at most b blocks, tests)
+    int64_t pgrid = env_i("CVD_K1S_PERSIST", 1) != 0 ? M.rtc_persist_grid : 0;
+    if (const int pb = env_i("CVD_K1S_PERSIST_BLOCKS", 0); pb > 0) pgrid = std::min<int64_t>(pgrid, pb);
+    if (M.rtc_bs && M.d_wq && pgrid > 0 && (int64_t)rgrid > pgrid) {
       static std::atomic<uint32_t> seq{0};
       a.wq = M.d_wq + (seq.fetch_add(1u) % kWqRing);
       HIP_CHECK(hipMemsetAsync(a.wq, 0, sizeof(uint32_t), (hipStream_t)stream));
-      rgrid = (unsigned)M.rtc_persist_grid;
+      rgrid = (unsigned)pgrid;
     }
     HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M.rtc_fn, rgrid, 1, 1, blk, 1, 1, lds,
                                     (hipStream_t)stream, args, nullptr));
@@ -1934,10 +1937,9 @@ int cvd::upload_model(cvd_model& M, int device) {
     M.rtc_ldsf = false;
     M.rtc_block = kBlock;
   }
-  // persistent launches of k1s (CVD_K1S_PERSIST=0: one block per 64 x (block / 64) sequences):
-  // as many blocks as the device keeps resident
+  // persistent launches of k1s: as many blocks as the device keeps resident
   M.rtc_persist_grid = 0;
-  if (M.rtc_fn && M.rtc_bs && env_i("CVD_K1S_PERSIST", 1) != 0) {
+  if (M.rtc_fn && M.rtc_bs) {
     int nb = 0, ncu = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (hipFunction_t)M.rtc_fn, M.rtc_block,
                                                            rtc_dyn_lds(M)) == hipSuccess &&

@@ -392,7 +392,7 @@ class Detector:
         if T <= 0:
             return {"counts": counts, "sums": np.zeros((0, 4))} if return_sums else {"counts": counts}
         if fused:
-            sums = torch.empty((T, 4), dtype=torch.float64, device=self.device) if return_sums else None
+            sums = torch.full((T, 4), float("nan"), dtype=torch.float64, device=self.device) if return_sums else None
             flags = _lib.DETECT_EARLY_DECISION if early_decision else 0
             _lib.check(_lib.lib().cvd_mc_fused(model.handle, g1.c, g2.c, float(p), int(N),
                                                int(seed) & 0xFFFFFFFFFFFFFFFF, int(trial_begin), int(trial_end),
@@ -427,7 +427,9 @@ class Detector:
             r = self.stream_buffer(N, 2 * Tb)
             self.generate(g1, N, p, seed, tag, 2 * b, 2, Tb, out=r, q0=0, pitch=2 * Tb, stream=stream)
             self.generate(g2, N, p, seed, tag, 2 * b + 1, 2, Tb, out=r, q0=Tb, pitch=2 * Tb, stream=stream)
-            sums = torch.empty((2 * Tb, 2), dtype=torch.float64, device=self.device)
+            # NaN-filled: a sequence the kernel never wrote cannot pass for a result (the
+            # allocator hands back the previous call's buffer)
+            sums = torch.full((2 * Tb, 2), float("nan"), dtype=torch.float64, device=self.device)
             self.detect(model, r, N, 2 * Tb, Tb, sums=sums, counts=counts, path=path, stream=stream)
             s = sums.cpu().numpy()
             out.append(np.concatenate([s[:Tb], s[Tb:]], axis=1))

@@ -45,11 +45,11 @@ def test_multi_equals_separate_launches(pkg):
         assert len({inf[i]["lds_filter"] for i in g}) == 1
     ref_s, ref_c = [], []
     for m, r, t in zip(models, bufs, T):
-        s = torch.empty((2 * t, 2), dtype=torch.float64, device=det.device)
+        s = torch.full((2 * t, 2), float("nan"), dtype=torch.float64, device=det.device)
         c = det.detect(m, r, N, 2 * t, t, sums=s)
         ref_s.append(s.cpu().numpy())
         ref_c.append(c.cpu().tolist())
-    sums = [torch.empty((2 * t, 2), dtype=torch.float64, device=det.device) for t in T]
+    sums = [torch.full((2 * t, 2), float("nan"), dtype=torch.float64, device=det.device) for t in T]
     cnts = [torch.zeros(2, dtype=torch.int64, device=det.device) for _ in T]
     det.detect_multi(models, bufs, N, [2 * t for t in T], T, cnts, sums=sums)
     for i in range(len(ps)):
@@ -68,7 +68,7 @@ def test_multi_equals_c_oracle(pkg):
     ps = [0.02, 0.05, 0.1, 0.15]
     N, T, lo = 2000, [96] * 4, 1_000_000
     cc, det, models, bufs = _setup(pkg, ps, N, T, lo=lo, ll=200_000)
-    sums = [torch.empty((2 * t, 2), dtype=torch.float64, device=det.device) for t in T]
+    sums = [torch.full((2 * t, 2), float("nan"), dtype=torch.float64, device=det.device) for t in T]
     cnts = [torch.zeros(2, dtype=torch.int64, device=det.device) for _ in T]
     det.detect_multi(models, bufs, N, [2 * t for t in T], T, cnts, sums=sums)
     c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)

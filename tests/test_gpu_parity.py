@@ -383,7 +383,7 @@ def test_m6_batch_beyond_32bit_offsets(pkg, dev):
     r = det.stream_buffer(N, 2 * B)
     det.generate(cc["gen1"], N, p, seed, tag, 0, 2, B, out=r, q0=0, pitch=2 * B)
     det.generate(cc["gen2"], N, p, seed, tag, 1, 2, B, out=r, q0=B, pitch=2 * B)
-    sums = torch.empty((2 * B, 2), dtype=torch.float64, device=r.device)
+    sums = torch.full((2 * B, 2), float("nan"), dtype=torch.float64, device=r.device)
     det.detect(model, r, N, 2 * B, B, sums=sums)
     s = sums[torch.tensor([B - 2, B - 1, 2 * B - 2, 2 * B - 1], device=r.device)].cpu().numpy()
     del r, sums

@@ -173,3 +173,24 @@ def test_walk_guard_flag_is_reported(pkg, monkeypatch):
     with pytest.raises(pkg.CvdError, match="scheduler guard"):
         det.run_trials(model, cc["gen1"], cc["gen2"], 2000, 0.01, 7, 0, 256, return_sums=True)
     assert model.device_error() == 0          # the flag was read and cleared
+
+
+@pytest.mark.parametrize("p", [0.01, 0.02, 0.05, 0.2])
+def test_persistent_launch_equals_block_launch(pkg, monkeypatch, p):
+    """The k1s work-queue launch (cvd_k1s.h k1s_body: one block per resident slot, waves
+    taking 64 sequences at a time) gives the block launch's sums and counts, lockstep and walk
+    mode, trial counts that leave a partial last unit and an odd number of units.  Capping it
+    at 2 blocks (CVD_K1S_PERSIST_BLOCKS) makes these small launches go through the queue."""
+    cc, det = _m6(pkg)
+    model = det.model(p, 200_000, 200, 1.0, SEED)
+    for N, t0, t1 in [(1237, 0, 1500), (2000, 77, 77 + 2111)]:
+        monkeypatch.setenv("CVD_K1S_PERSIST", "0")
+        ref, rc = _sums(det, model, cc, N, p, t0, t1)
+        monkeypatch.setenv("CVD_K1S_PERSIST", "1")
+        monkeypatch.setenv("CVD_K1S_PERSIST_BLOCKS", "2")
+        got, gc = _sums(det, model, cc, N, p, t0, t1)
+        monkeypatch.delenv("CVD_K1S_PERSIST_BLOCKS")
+        assert not np.isnan(got).any()
+        assert np.array_equal(got, ref), (p, N)
+        assert gc == rc
+    assert model.device_error() == 0
