@@ -514,8 +514,9 @@ void build_hash(cvd_model& Mo) {
   // so that the specialised kernel keeps the whole filter in LDS (ldsf_preferred,
   // cvd_kernels.hip): up to 4 keys per two-word block, ~0.06% false positives, against an
   // L2 read per H2 step.
-  const bool ldsf = walk_preferred(Mo) && Mo.n_rows <= ldsf_max_rows() && !std::getenv("CVD_NO_LDSF");
-  int fscale = 0, fmax_log2 = ldsf ? ldsf_log2() : 19;
+  const bool bsp = bitslice_preferred(Mo);
+  const bool ldsf = walk_preferred(Mo) && Mo.n_rows <= ldsf_max_rows(bsp) && !std::getenv("CVD_NO_LDSF");
+  int fscale = 0, fmax_log2 = ldsf ? ldsf_log2(bsp) : 19;
   if (const char* e = std::getenv("CVD_FILTER_SCALE")) fscale = std::max(-3, std::min(3, std::atoi(e)));
   if (const char* e = std::getenv("CVD_FILTER_MAX_LOG2")) fmax_log2 = std::max(8, std::min(28, std::atoi(e)));
   while ((fscale >= 0 ? fcap >> fscale : fcap << -fscale) < Mo.n_rows && fcap < ((int64_t)1 << fmax_log2)) fcap <<= 1;
@@ -782,13 +783,16 @@ void build_bmp(cvd_model& Mo, const Tabs& T) {
 
 }  // namespace
 
-int cvd::ldsf_log2() {
+int cvd::ldsf_log2(bool bs) {
+  // the bit-sliced kernel's persistent blocks hold a 128-KiB filter one block per CU (p = 0.01:
+  // 1,440 vs 1,511 ms per launch with 64 KiB in two 512-thread blocks, profiles/r05l); the
+  // nibble kernel keeps 64 KiB (profiles/r03x)
   const char* e = std::getenv("CVD_LDSF_LOG2");
-  return e && *e ? std::max(13, std::min(15, std::atoi(e))) : kLdsFilterLog2;
+  return e && *e ? std::max(13, std::min(15, std::atoi(e))) : (bs ? 15 : kLdsFilterLog2);
 }
-int64_t cvd::ldsf_max_rows() {
+int64_t cvd::ldsf_max_rows(bool bs) {
   const char* e = std::getenv("CVD_LDSF_MAX_ROWS");
-  return e && *e ? (int64_t)std::atoll(e) : (kLdsFilterMaxRows << (ldsf_log2() - kLdsFilterLog2));
+  return e && *e ? (int64_t)std::atoll(e) : kLdsFilterMaxRows << std::max(0, ldsf_log2(bs) - (bs ? 15 : kLdsFilterLog2));
 }
 
 bool cvd::bs_pf_preferred(const cvd_model& M, bool ldsf) {

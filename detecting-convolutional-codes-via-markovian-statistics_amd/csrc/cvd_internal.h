@@ -139,11 +139,11 @@ constexpr int kLdsFilterLog2 = 14;
 constexpr int64_t kLdsFilterMaxRows = 32768;
 // the LDS filter's size (2^log2 words) and row cap: kLdsFilterLog2 / kLdsFilterMaxRows unless
 // CVD_LDSF_LOG2 (13..15; 15: 128 KiB, 1,024-thread blocks) / CVD_LDSF_MAX_ROWS set them
-int ldsf_log2();
-// the k1s LDS pre-filter (cvd_bitslice.h kBsPfLog2Bits: 128 KiB of dynamic LDS, 1,024-thread
+int ldsf_log2(bool bs);
+// the k1s LDS pre-filter (cvd_keys.h kBsPfLog2Bits: 128 KiB of dynamic LDS, 1,024-thread
 // blocks) for bit-sliced models without the LDS-resident filter, unless CVD_BS_PF=0
 bool bs_pf_preferred(const cvd_model& M, bool ldsf);
-int64_t ldsf_max_rows();
+int64_t ldsf_max_rows(bool bs);
 bool ldsf_preferred(const cvd_model& M);
 int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
                     uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,

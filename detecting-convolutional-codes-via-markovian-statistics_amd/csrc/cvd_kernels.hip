@@ -1727,8 +1727,8 @@ int cvd::explicit_kernel_of(const cvd_model& M) {
 // threads with the global filter 570.9 / 668.7, 512 threads 541.6 / 625.7).  CVD_NO_LDSF=1
 // keeps the filter in global memory.
 bool cvd::ldsf_preferred(const cvd_model& M) {
-  return !std::getenv("CVD_NO_LDSF") && walk_preferred(M) && M.n_rows <= ldsf_max_rows() &&
-         M.fcap <= ((int64_t)1 << ldsf_log2()) && M.h_filt_lds.size() == (size_t)M.fcap;
+  return !std::getenv("CVD_NO_LDSF") && walk_preferred(M) && M.n_rows <= ldsf_max_rows(M.bs) &&
+         M.fcap <= ((int64_t)1 << ldsf_log2(M.bs)) && M.h_filt_lds.size() == (size_t)M.fcap;
 }
 
 bool cvd::walk_preferred(const cvd_model& M, bool early) {
