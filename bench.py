@@ -754,7 +754,8 @@ def run_c4(a, pkg, world, rank, local, dist):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": ("u32 bit-planes (metrics, four planes of the 64 states) + f64 (log-likelihood sums)"
-                  if info.get("explicit_kernel") == 5 else "u16x2 (metrics) + f64 (log-likelihood sums)"),
+                  if models[p_grid[0]].info().get("explicit_kernel") == 5
+                  else "u16x2 (metrics) + f64 (log-likelihood sums)"),
         "data": "synthetic: Philox4x32-10 encoder inputs and BSC(p) flips (build spec), learned P̂1",
         "config": {"name": "c4", "workload": f"m6 pair {cc['gen1']} vs {cc['gen2']}, N in {Ns} x p {p_grid}, "
                                              f"{T} trials per grid point ({total} total), one step = one grid point",
