@@ -332,13 +332,23 @@ CVD_HD void bs_step_core(const bs_u32 (&R)[2][4], const bs_u32 (&e0)[2], const b
   c = 1u + (sym == 0u ? 1u : 0u) + ((kUni && (dh[0] | dh[1]) == 0u) ? 2u : 0u);
 }
 
-// canonical digest hash of planes N at phase PH (cvd_keys.h key_hash over the two words)
+// the bit-sliced tables' key hash of the canonical digest (lo, hi): key_hash's two-word
+// fold without its start constant (which only shifted the sum; LLVM added it as one more
+// 64-bit VALU op) -- acc = lo K0 + hi K1, x = acc_lo ^ acc_hi, (ph, pl) = x K2
+CVD_HD void bs_key_hash(bs_u32 lo, bs_u32 hi, bs_u32& ph, bs_u32& pl) {
+  const bs_u64 acc = mul_wide(lo, 0x85EBCA77u) + mul_wide(hi, 0x85EBCA77u + 0x6A09E668u);
+  const bs_u32 x = (bs_u32)acc ^ (bs_u32)(acc >> 32);
+  const bs_u64 p = mul_wide(x, 0x85EBCA6Bu);
+  ph = (bs_u32)(p >> 32);
+  pl = (bs_u32)p;
+}
+
+// canonical digest hash of planes N at phase PH
 template <int PH>
 CVD_HD void bs_digest_hash(const bs_u32 (&N)[2][4], bs_u32& ph, bs_u32& pl) {
   bs_u32 lo = N[0][0] ^ N[0][1], hi = N[1][0] ^ N[1][1];
   bs_canon<PH>(lo, hi);
-  const bs_u32 w[2] = {lo, hi};
-  key_hash(w, 2, ph, pl);
+  bs_key_hash(lo, hi, ph, pl);
 }
 
 }  // namespace cvd

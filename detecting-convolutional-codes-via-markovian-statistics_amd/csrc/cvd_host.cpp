@@ -641,7 +641,7 @@ void build_hash(cvd_model& Mo) {
     parallel_for(Mo.n_rows, [&](int64_t i, int) {
       uint32_t z[2];
       bs_digest(Mo.keys.data() + (size_t)i * M, z);
-      key_hash(z, 2, bph[(size_t)i], bpl[(size_t)i]);
+      bs_key_hash(z[0], z[1], bph[(size_t)i], bpl[(size_t)i]);
     });
     std::vector<uint8_t> used((size_t)bcap, 0);
     std::vector<int64_t> bslot((size_t)Mo.n_rows);

@@ -72,6 +72,7 @@ struct BsCursor {
   int32_t slot, pnx;
   uint32_t hs, hsn, fb, fw, fb1, fw1, pc;   // hs: home slot of D_{t-1}'s lookup, hsn: of D_t's
   bool cand;
+  bool pfpos = true;     // D_t's pre-filter bit (CVD_K1S_PF; hash_ahead -> resolve)
   bool h2wave = false;   // (CVD_K1S_ABL timing studies: the wave holds H2 sequences only)
   double plp;
   uint32_t pkey[8];
@@ -132,7 +133,8 @@ struct BsCursor {
   // filter positive: the home slot's image of phase PH and its record for word r
   template <int PH>
   __device__ void mid(const ExpArgs& a, uint32_t r) {
-    cand = slot == -2 && ((fb & ~fw) | (fb1 & ~fw1)) == 0u;
+    // (two v_bitop3: the compiler's form was six VALU)
+    cand = slot == -2 && cvd::bs_bop3<cvd::kTtAndNotOr>(fb1, fw1, cvd::bs_bop3<cvd::kTtAndNotOr>(fb, fw, 0u)) == 0u;
     if (cand) {
       const uint32_t so = slot_off(hs);
       load_image(a.hkey, so + 32u * PH, pkey);
@@ -158,7 +160,7 @@ struct BsCursor {
   template <int PH>
   __device__ double resolve(const ExpArgs& a, const uint32_t (&R)[2][4], uint32_t r, double lpu) {
     double lpv = lpu;
-    int32_t ns = -2;
+    int32_t ns = pfpos ? -2 : -1;   // D_t's lookup pending, or settled by the pre-filter
     const bool known = slot >= 0;
     if (known) {
       lpv = plp; ns = pnx;
@@ -213,16 +215,19 @@ struct BsCursor {
       fb1 = pp.y;
 #if CVD_K1S_PF
       // the pre-filter bit of D_t (LDS): clear -- D_t is not a row -- and the lane reads filter
-      // word 0 like a lane that needs no lookup, with an all-ones pattern that word 0 cannot
-      // match (a match would only cost a wasted candidate test: the compare is exact)
-      const uint32_t pfw = *reinterpret_cast<const uint32_t*>(
-          reinterpret_cast<const char*>(dyn_lds()) + ((pl >> (32 - cvd::kBsPfLog2Bits + 5 - 2)) & ~3u));
-      const bool pos = ((pfw >> ((pl >> (32 - cvd::kBsPfLog2Bits)) & 31u)) & 1u) != 0u;
-      if (!pos) { fb = ~0u; fb1 = ~0u; }
+      // word 0 like a lane that needs no lookup; the resolve then marks D_t "not a row" (-1)
+      // instead of "pending" (-2), so no candidate test follows
+      const uint32_t pfw = reinterpret_cast<const uint32_t*>(dyn_lds())[__builtin_amdgcn_ubfe(
+          pl, 32 - cvd::kBsPfLog2Bits + 5, cvd::kBsPfLog2Bits - 5)];
+      // (bit (pl >> (32 - kBsPfLog2Bits)) mod 32 of the word: the extract takes the offset's
+      // low five bits)
+      const bool pos = __builtin_amdgcn_ubfe(pfw, pl >> (32 - cvd::kBsPfLog2Bits), 1u) != 0u;
+      pfpos = pos;
 #else
       constexpr bool pos = true;
 #endif
-      const uint32_t fo = slot < 0 && pos && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & a.fmask4) : 0u;
+      uint32_t fo = slot < 0 && pos && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & a.fmask4) : 0u;
+      asm volatile("" : "+v"(fo));   // a plain 32-bit offset: the SGPR-base load form
 #if CVD_K1B_LDSF
       const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + fo);
 #else

@@ -4,7 +4,7 @@
 // a BSC) and every layout phase it checks: the new planes equal the phase-(f+1) image of
 // the reference step's D_t; mu equals the step's minimum; c equals the number of words
 // r' with step(D, r') == D_t (the T_ref count, Pd_plotter.py:89-99); the digest hash of
-// the new planes equals the host key of D_t (bs_digest + key_hash), and bs_canon<f> maps
+// the new planes equals the host key of D_t (bs_digest + bs_key_hash), and bs_canon<f> maps
 // every phase-f digest image to the phase-0 one.  TEST INFRASTRUCTURE ONLY.
 #include <cstdio>
 #include <cstdlib>
@@ -164,7 +164,7 @@ int main(int argc, char** argv) {
       if (c != cref) return fail("T_ref count", t, ph);
       bs_u32 z[2], kph, kpl;
       bs_digest(Dn, z);
-      key_hash(z, 2, kph, kpl);
+      bs_key_hash(z[0], z[1], kph, kpl);
       if (kph != hph || kpl != hpl) return fail("digest hash", t, ph);
       for (int s = 0; s < 64; ++s) dmax = Dn[s] > dmax ? Dn[s] : dmax;
       c_counts[c]++;
