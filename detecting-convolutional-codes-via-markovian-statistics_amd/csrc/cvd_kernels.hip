@@ -1734,7 +1734,11 @@ bool cvd::ldsf_preferred(const cvd_model& M) {
 bool cvd::walk_preferred(const cvd_model& M, bool early) {
   const int e = env_i("CVD_WALK", -1);
   if (e >= 0) return e != 0;
-  return !early && M.kind == 1 && M.learn_len_eff > 0 && 10 * M.n_rows < M.learn_len_eff;
+  // the bit-sliced kernel's lockstep steps are cheaper, so it walks only below 1/20: p = 0.02
+  // (70,134 rows / 10^6) runs 1,584 ms lockstep against 1,703 walking, p = 0.01 (29,626) 1,433
+  // walking against 1,534 (profiles/r05r_p*/)
+  const int64_t ratio = bitslice_preferred(M) ? 20 : 10;
+  return !early && M.kind == 1 && M.learn_len_eff > 0 && ratio * M.n_rows < M.learn_len_eff;
 }
 
 constexpr uint32_t kWqRing = 64;   // work-queue counters per model (persistent k1s launches)

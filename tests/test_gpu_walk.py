@@ -88,14 +88,16 @@ def test_walk_early_decision_counts(pkg, monkeypatch, p):
 
 
 def test_walk_flag_follows_row_share(pkg, monkeypatch):
-    """cvd_model_info.walk: on where the model's rows / learn_len < 1/10 (H1 stays in rows),
-    off elsewhere and for dense models; CVD_WALK forces it."""
+    """cvd_model_info.walk: on where the model's rows / learn_len < 1/20 (H1 stays in rows;
+    the bit-sliced kernel's threshold), off elsewhere and for dense models; CVD_WALK forces it."""
     cc, det = _m6(pkg)
     monkeypatch.delenv("CVD_WALK", raising=False)
     lo = det.model(0.01, 1_000_000, 200, 1.0, SEED).info()
     hi = det.model(0.1, 1_000_000, 200, 1.0, SEED).info()
-    assert 10 * lo["n_rows"] < lo["learn_len_eff"] and lo["walk"] == 1
-    assert 10 * hi["n_rows"] >= hi["learn_len_eff"] and hi["walk"] == 0
+    assert 20 * lo["n_rows"] < lo["learn_len_eff"] and lo["walk"] == 1
+    assert 20 * hi["n_rows"] >= hi["learn_len_eff"] and hi["walk"] == 0
+    mid = det.model(0.02, 1_000_000, 200, 1.0, SEED).info()   # 70,134 rows: lockstep
+    assert 20 * mid["n_rows"] >= mid["learn_len_eff"] and mid["walk"] == 0
     monkeypatch.setenv("CVD_WALK", "1")
     assert det.model(0.1, 1_000_000, 200, 1.0, SEED).info()["walk"] == 1
     m2 = pkg.CONFIG_CODES["m2"]
@@ -175,14 +177,15 @@ def test_walk_guard_flag_is_reported(pkg, monkeypatch):
     assert model.device_error() == 0          # the flag was read and cleared
 
 
-@pytest.mark.parametrize("p", [0.01, 0.02, 0.05, 0.2])
-def test_persistent_launch_equals_block_launch(pkg, monkeypatch, p):
+@pytest.mark.parametrize("p,walk", [(0.01, "1"), (0.02, "1"), (0.05, "0"), (0.2, "0")])
+def test_persistent_launch_equals_block_launch(pkg, monkeypatch, p, walk):
     """The k1s work-queue launch (cvd_k1s.h k1s_body: one block per resident slot, waves
     taking 64 sequences at a time) gives the block launch's sums and counts, lockstep and walk
     mode, trial counts that leave a partial last unit and an odd number of units.  Capping it
     at 2 blocks (CVD_K1S_PERSIST_BLOCKS) makes these small launches go through the queue."""
     cc, det = _m6(pkg)
     model = det.model(p, 200_000, 200, 1.0, SEED)
+    monkeypatch.setenv("CVD_WALK", walk)
     for N, t0, t1 in [(1237, 0, 1500), (2000, 77, 77 + 2111)]:
         monkeypatch.setenv("CVD_K1S_PERSIST", "0")
         ref, rc = _sums(det, model, cc, N, p, t0, t1)

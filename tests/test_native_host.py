@@ -158,20 +158,21 @@ def test_directory_sizing(pkg, monkeypatch):
 
 def test_walk_and_lds_filter_flags(pkg, monkeypatch):
     """cvd_model_info.walk / lds_filter before upload (cvd_kernels.hip walk_preferred,
-    ldsf_preferred): a model whose rows / learn_len < 1/10 walks, and one of <= 32,768 rows
+    ldsf_preferred): a model whose rows / learn_len < 1/20 walks (the bit-sliced kernel's
+    threshold; 1/10 for the nibble kernel), and one of <= 32,768 rows
     also keeps its Bloom filter in LDS; CVD_NO_LDSF=1 (read at build) turns that off and
     CVD_WALK=0 both."""
     taps = [[[1, 0, 1, 1, 0, 1, 1]], [[1, 1, 1, 1, 0, 0, 1]]]
     code = pkg.Code(taps, 6, 1, 2)
     for v in ("CVD_WALK", "CVD_NO_LDSF"):
         monkeypatch.delenv(v, raising=False)
-    inf = pkg.Model(code, 0.01, 200_000, 200, 1.0, 7).info()
-    assert 10 * inf["n_rows"] < inf["learn_len_eff"] and inf["n_rows"] <= 32768
+    inf = pkg.Model(code, 0.01, 300_000, 200, 1.0, 7).info()
+    assert 20 * inf["n_rows"] < inf["learn_len_eff"] and inf["n_rows"] <= 32768
     assert inf["walk"] == 1 and inf["lds_filter"] == 1
     hi = pkg.Model(code, 0.1, 20_000, 200, 1.0, 7).info()
     assert hi["walk"] == 0 and hi["lds_filter"] == 0
     monkeypatch.setenv("CVD_NO_LDSF", "1")
-    assert pkg.Model(code, 0.01, 200_000, 200, 1.0, 7).info()["lds_filter"] == 0
+    assert pkg.Model(code, 0.01, 300_000, 200, 1.0, 7).info()["lds_filter"] == 0
     monkeypatch.delenv("CVD_NO_LDSF")
     monkeypatch.setenv("CVD_WALK", "0")
     off = pkg.Model(code, 0.01, 200_000, 200, 1.0, 7).info()
