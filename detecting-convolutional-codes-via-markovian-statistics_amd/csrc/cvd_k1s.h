@@ -43,6 +43,12 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #ifndef CVD_K1S_T2
 #define CVD_K1S_T2 0
 #endif
+// cursor forms (timing studies): bit 0 -- a pre-filter negative marks D_t "not a row" at the
+// resolve (else: an all-ones pattern that filter word 0 cannot match); bit 1 -- the filter
+// offset through an empty asm (the SGPR-base load form)
+#ifndef CVD_K1S_TRIM
+#define CVD_K1S_TRIM 3
+#endif
 constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
 
 // LDS: per (phase, y) two uint4 {e0, e1, ez, 0} of word 0 and word 1 (cvd::bs_eplanes)
@@ -222,12 +228,17 @@ struct BsCursor {
       // (bit (pl >> (32 - kBsPfLog2Bits)) mod 32 of the word: the extract takes the offset's
       // low five bits)
       const bool pos = __builtin_amdgcn_ubfe(pfw, pl >> (32 - cvd::kBsPfLog2Bits), 1u) != 0u;
-      pfpos = pos;
+      if (CVD_K1S_TRIM & 1) {
+        pfpos = pos;
+      } else if (!pos) {
+        fb = ~0u;
+        fb1 = ~0u;
+      }
 #else
       constexpr bool pos = true;
 #endif
       uint32_t fo = slot < 0 && pos && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & a.fmask4) : 0u;
-      asm volatile("" : "+v"(fo));   // a plain 32-bit offset: the SGPR-base load form
+      if (CVD_K1S_TRIM & 2) asm volatile("" : "+v"(fo));   // a plain 32-bit offset: the SGPR-base load form
 #if CVD_K1B_LDSF
       const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + fo);
 #else
