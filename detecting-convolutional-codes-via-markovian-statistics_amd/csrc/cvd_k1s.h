@@ -43,11 +43,12 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #ifndef CVD_K1S_T2
 #define CVD_K1S_T2 0
 #endif
-// cursor forms (timing studies): bit 0 -- a pre-filter negative marks D_t "not a row" at the
-// resolve (else: an all-ones pattern that filter word 0 cannot match); bit 1 -- the filter
-// offset through an empty asm (the SGPR-base load form)
+// cursor forms (timing studies; both off: profiles/r05t, p = 0.2 / 0.05 1,949 / 1,953 ms per
+// launch against 1,970 / 1,979 with both): bit 0 -- a pre-filter negative marks D_t "not a
+// row" at the resolve (else: an all-ones pattern that filter word 0 cannot match); bit 1 --
+// the filter offset through an empty asm (the SGPR-base load form)
 #ifndef CVD_K1S_TRIM
-#define CVD_K1S_TRIM 3
+#define CVD_K1S_TRIM 0
 #endif
 constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
 
