@@ -52,6 +52,22 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #endif
 constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
 
+// The lockstep lanes read each 16-B stream chunk once: non-temporal loads (CVD_K1S_NT_STREAM,
+// default on) so that the 131 GB per launch do not evict the row tables' lines from L2 (p = 0.1
+// / 0.15 2,074 / 2,040 -> 2,041-2,049 / 2,008 ms, profiles/r05y)
+#ifndef CVD_K1S_NT_STREAM
+#define CVD_K1S_NT_STREAM 1
+#endif
+typedef unsigned int bs_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 stream_load(const uint4* p) {
+  if constexpr (CVD_K1S_NT_STREAM != 0) {
+    const bs_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const bs_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
+}
+
 // LDS: per (phase, y) two uint4 {e0, e1, ez, 0} of word 0 and word 1 (cvd::bs_eplanes)
 __device__ __forceinline__ uint4* bs_etab_lds() {
   __shared__ uint4 s_et[6 * 4 * 2];
@@ -290,6 +306,8 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   const size_t cstride = (size_t)a.nseq * 4;
   auto load_word = [&](uint32_t wi) -> uint32_t {
     if (wi >= nwords) return 0u;
+    // (a plain load: walk mode reads a 16-B chunk's four words one at a time, and non-temporal
+    // lines were gone before the next word -- p = 0.01 1,411 -> 1,489 ms, profiles/r05y)
     return a.r[(size_t)(wi >> 2) * cstride + (size_t)(qwave + lane_id()) * 4 + (wi & 3u)];
   };
   uint32_t pos = 0u, curw = 0u, nxtw = 0u;
@@ -485,7 +503,8 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     uint32_t c4[4];
     auto load_chunk = [&](int64_t ci) {
       const uint32_t* rb = a.r + (size_t)ci * cstride + (size_t)qwave * 4;
-      const uint4 v = 4 * ci < nwords ? *reinterpret_cast<const uint4*>(rb + lane_id() * 4u) : make_uint4(0u, 0u, 0u, 0u);
+      const uint4 v = 4 * ci < nwords ? stream_load(reinterpret_cast<const uint4*>(rb + lane_id() * 4u))
+                                      : make_uint4(0u, 0u, 0u, 0u);
       c4[0] = v.x; c4[1] = v.y; c4[2] = v.z; c4[3] = v.w;
     };
     auto pick = [&](int64_t wi) -> uint32_t {
