@@ -10,9 +10,11 @@
 // planes and, for a lane whose new vector must be hashed, the canonical digest hash.  The
 // row tables are the bit-sliced ones (cvd_host.cpp build_hash with bs): the Bloom filter
 // over the digest hash, 256-byte directory slots {six phase images, the row's record}, six
-// images per learned row by row id (walk mode) and the usual dense records.  The layout
-// phase is compile-time in the lockstep loop (six steps per iteration) and wave-uniform in
-// walk mode.
+// images per learned row by row id (walk mode) and the usual dense records; in front of the
+// L2 filter, a 2^20-bit pre-filter in LDS (CVD_K1S_PF).  The layout phase is compile-time in
+// the lockstep loop (six steps per iteration) and wave-uniform in walk mode.  A launch over
+// more sequences than stay resident is persistent: one block per slot, each wave taking 64
+// sequences at a time from a work queue (k1s_body).
 #pragma once
 
 #ifndef CVD_K1B_BITSLICE
@@ -37,9 +39,10 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #define CVD_K1S_PF 0
 #endif
 // two-step records for the lockstep lanes that walk learned rows (CVD_K1S_T2=1 with the
-// model's t2 table, CVD_BS_T2=1): one load per two steps.  Off by default: +1.5% at p = 0.05,
-// -0.8% to -2.6% at p >= 0.1 with the pre-filter (profiles/r05j: the 512-B-per-row table
-// spreads the walks over 8x the lines), and its 4 VGPRs
+// model's t2 table, CVD_BS_T2=1): one load per two steps.  Off: +1.5% at p = 0.05, -0.8% to
+// -2.6% at p >= 0.1 in block launches (profiles/r05j: the 512-B-per-row table spreads the
+// walks over 8x the lines), and with the persistent launch its 4 VGPRs spill: -14% / -22% at
+// p = 0.05 / 0.1 (profiles/r05aa)
 #ifndef CVD_K1S_T2
 #define CVD_K1S_T2 0
 #endif
