@@ -264,7 +264,7 @@ def main():
     main = torch.cuda.current_stream()
     gstream = torch.cuda.Stream(device=det.device) if a.overlap else main
     use_multi = sweep_all and bool(a.multi) and not (a.overlap or a.fused or parity)
-    groups = (det.multi_groups([models[p] for p in p_grid]) if use_multi
+    groups = (det.multi_groups([models[p] for p in p_grid], [2 * B] * len(p_grid)) if use_multi
               else [[j] for j in range(per_step)])      # positions within a step's units
     nq = 1 if (a.overlap or not sweep_all) else max(1, min(a.group_streams, len(groups)))
     queues = [main] + [torch.cuda.Stream(device=det.device) for _ in range(nq - 1)]

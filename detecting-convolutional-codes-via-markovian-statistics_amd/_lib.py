@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CVD_LIB_PATH: another build of the same ABI (A/B builds, profiles/build_ab.sh)
 LIB_PATH = os.environ.get("CVD_LIB_PATH") or os.path.join(_HERE, "lib", "libcvd.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5
 DETECT_EARLY_DECISION = 0x100   # OR'ed into path: counts only, stop once every decision is certain
@@ -42,7 +42,7 @@ class cvd_model_info(ctypes.Structure):
                 ("max_probe", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("logp1_unseen", ctypes.c_double), ("explicit_kernel", ctypes.c_int32),
                 ("mc_fused", ctypes.c_int32), ("walk", ctypes.c_int32), ("lds_filter", ctypes.c_int32),
-                ("pad0", ctypes.c_int32), ("multi_variant", ctypes.c_int64)]
+                ("pad0", ctypes.c_int32), ("multi_variant", ctypes.c_int64), ("persist_seqs", ctypes.c_int64)]
 
 
 KERNEL_NAMES = {0: "none", 1: "detect_explicit_kernel (generic explicit path)",

@@ -15,6 +15,8 @@ bool cvd::mc_fused_preferred(const cvd_model&) { return false; }
 bool cvd::walk_preferred(const cvd_model&, bool) { return false; }
 bool cvd::ldsf_preferred(const cvd_model&) { return false; }
 int64_t cvd::multi_variant(const cvd_model&) { return 0; }
+int64_t cvd::persist_seqs(const cvd_model&) { return 0; }
+int64_t cvd::persist_grid(const cvd_model&, int64_t) { return 0; }
 int cvd::device_learn_sparse(const CodeDesc&, int64_t, int64_t, uint64_t, double, int, void*, std::vector<uint8_t>&,
                              std::vector<int64_t>&, int64_t&, LearnStats*) {
   cvd::set_error("no device in the host sanitizer build");

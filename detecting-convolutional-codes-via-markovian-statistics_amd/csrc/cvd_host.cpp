@@ -1205,6 +1205,7 @@ extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
                                      : (Mo->k1b_ok && Mo->hcap > 0 && ldsf_preferred(*Mo) ? 1 : 0);
   info->pad0 = 0;
   info->multi_variant = multi_variant(*Mo);
+  info->persist_seqs = persist_seqs(*Mo);
   return CVD_OK;
 }
 

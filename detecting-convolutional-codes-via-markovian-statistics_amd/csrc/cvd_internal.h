@@ -168,6 +168,10 @@ bool explicit_supported(int m, int k, int n);
 bool bitslice_preferred(const cvd_model& M);
 // id of the multi-model launch variant (cvd_model_info.multi_variant; cvd_kernels.hip)
 int64_t multi_variant(const cvd_model& M);
+// sequences above which a launch of the model is persistent (cvd_model_info.persist_seqs; 0:
+// never), and the block count of such a launch over nseq sequences (0: a block launch)
+int64_t persist_seqs(const cvd_model& M);
+int64_t persist_grid(const cvd_model& M, int64_t nseq);
 
 // P̂1 learning chain on the GPU (cvd_learn.hip): identical outputs to the host chain.
 struct LearnStats {

@@ -1743,6 +1743,20 @@ bool cvd::walk_preferred(const cvd_model& M, bool early) {
 
 constexpr uint32_t kWqRing = 64;   // work-queue counters per model (persistent k1s launches)
 
+// the persistent launch's blocks (CVD_K1S_PERSIST=0: never; CVD_K1S_PERSIST_BLOCKS=b: at most b,
+// tests), and the sequences above which a launch is persistent
+static int64_t persist_cap(const cvd_model& M) {
+  if (!M.rtc_fn || !M.rtc_bs || !M.d_wq || M.rtc_persist_grid <= 0 || env_i("CVD_K1S_PERSIST", 1) == 0) return 0;
+  int64_t g = M.rtc_persist_grid;
+  if (const int pb = env_i("CVD_K1S_PERSIST_BLOCKS", 0); pb > 0) g = std::min<int64_t>(g, pb);
+  return g;
+}
+int64_t cvd::persist_seqs(const cvd_model& M) { return persist_cap(M) * M.rtc_block; }
+int64_t cvd::persist_grid(const cvd_model& M, int64_t nseq) {
+  const int64_t g = persist_cap(M);
+  return g > 0 && (nseq + M.rtc_block - 1) / M.rtc_block > g ? g : 0;
+}
+
 // dynamic LDS of the specialised kernel: the LDS-resident filter or the k1s pre-filter
 static unsigned rtc_dyn_lds(const cvd_model& M) {
   if (M.rtc_ldsf) return (unsigned)(M.fcap * sizeof(uint32_t));
@@ -1813,10 +1827,7 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
     // k1s over more blocks than stay resident: one block per resident slot, the waves taking
     // their sequences from a work queue (k1s_body); its counter, one of a ring per model, is
     // zeroed on the launch's stream
-    // (CVD_K1S_PERSIST=0: off; CVD_K1S_PERSIST_BLOCKS=b: at most b blocks, tests)
-    int64_t pgrid = env_i("CVD_K1S_PERSIST", 1) != 0 ? M.rtc_persist_grid : 0;
-    if (const int pb = env_i("CVD_K1S_PERSIST_BLOCKS", 0); pb > 0) pgrid = std::min<int64_t>(pgrid, pb);
-    if (M.rtc_bs && M.d_wq && pgrid > 0 && (int64_t)rgrid > pgrid) {
+    if (const int64_t pgrid = persist_grid(M, nseq); pgrid > 0) {
       static std::atomic<uint32_t> seq{0};
       a.wq = M.d_wq + (seq.fetch_add(1u) % kWqRing);
       HIP_CHECK(hipMemsetAsync(a.wq, 0, sizeof(uint32_t), (hipStream_t)stream));
@@ -2092,12 +2103,16 @@ extern "C" int cvd_detect_multi(const cvd_model* const* models, int32_t nm, cons
     if (rc) return rc;
   }
   int32_t i = 0;
+  // a model whose own launch is persistent (a batch past the resident capacity) runs alone:
+  // the work queue keeps a CU's waves busy to the end, which a merged block launch does not
+  // (cvd_model_info.persist_seqs)
+  auto merges = [&](int32_t k) { return multi_ok(*models[k]) && persist_grid(*models[k], nseq[k]) == 0; };
   while (i < nm) {
     const cvd_model& M = *models[i];
-    const bool mok = (base == CVD_PATH_AUTO || base == CVD_PATH_EXPLICIT) && multi_ok(M);
+    const bool mok = (base == CVD_PATH_AUTO || base == CVD_PATH_EXPLICIT) && merges(i);
     int32_t j = i + 1;
     if (mok)
-      while (j < nm && j - i < kMultiMax && multi_ok(*models[j]) && multi_same(M, *models[j])) ++j;
+      while (j < nm && j - i < kMultiMax && merges(j) && multi_same(M, *models[j])) ++j;
     int rc;
     if (mok && j - i > 1) {
       rc = launch_multi(models, i, j, d_r, N, nseq, n_h1, d_sums, d_counts, stream, early);

@@ -327,13 +327,17 @@ class Detector:
         return counts
 
     @staticmethod
-    def multi_groups(models):
+    def multi_groups(models, nseq=None):
         """Index runs of `models` that cvd_detect_multi merges into one launch (the same
         specialised kernel variant, as the library reports it: cvd_model_info.multi_variant;
-        at most 8 per launch) -- for per-launch timing."""
+        at most 8 per launch; a model whose launch over nseq[i] sequences is persistent,
+        nseq[i] > cvd_model_info.persist_seqs > 0, alone) -- for per-launch timing."""
         groups, cur, key = [], [], None
         for i, m in enumerate(models):
-            k = m.info()["multi_variant"] or None
+            inf = m.info()
+            k = inf["multi_variant"] or None
+            if k is not None and nseq is not None and 0 < inf["persist_seqs"] < int(nseq[i]):
+                k = None
             if cur and (k is None or k != key or len(cur) == 8 or os.environ.get("CVD_NO_MULTI")):
                 groups.append(cur)
                 cur = []

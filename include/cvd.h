@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 9
+#define CVD_ABI_VERSION 10
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -87,16 +87,22 @@ typedef struct cvd_model_info {
                               large tables is slower than the two-kernel pipeline) */
   int32_t walk;            /* 1: the specialised m = 6 kernel runs this model's H1 waves in walk mode
                               (learned-row steps from the row records, no ACS; sums unchanged): the
-                              model's rows / learn_len < 1/10, i.e. H1 stays in learned rows (CVD_WALK
-                              overrides; traces and, unless CVD_WALK=1, counts-only early decision
-                              run lockstep) */
-  int32_t lds_filter;      /* 1: the specialised kernel keeps this model's Bloom filter in LDS (walking
-                              models of <= 32,768 rows, filter built with 64 KiB, 512-thread blocks;
+                              model's rows / learn_len < 1/20 (bit-sliced kernel; 1/10 butterfly
+                              kernel), i.e. H1 stays in learned rows (CVD_WALK overrides; traces and,
+                              unless CVD_WALK=1, counts-only early decision run lockstep) */
+  int32_t lds_filter;      /* 1: the specialised kernel keeps this model's whole Bloom filter in LDS
+                              (walking models of <= 32,768 rows: 128 KiB in 1,024-thread blocks for the
+                              bit-sliced kernel, 64 KiB in 512-thread blocks for the butterfly kernel;
                               CVD_NO_LDSF=1 keeps it in global memory) */
   int32_t pad0;
   int64_t multi_variant;   /* nonzero: the specialised kernel variant this model runs in a
                               cvd_detect_multi launch; consecutive models with equal nonzero values
-                              share one launch (at most 8).  0: the model is detected on its own */
+                              share one launch (at most 8), except a model whose own launch would be
+                              persistent (persist_seqs below).  0: the model is detected on its own */
+  int64_t persist_seqs;    /* > 0: a launch of this model over more sequences than this (the bit-
+                              sliced kernel's resident capacity) is persistent -- one block per
+                              resident slot, waves taking 64 sequences at a time from a work queue
+                              -- and cvd_detect_multi launches it on its own (ABI 10).  0: never */
 } cvd_model_info;
 
 #define CVD_KERNEL_NONE 0       /* explicit path unsupported for this shape */

@@ -96,3 +96,38 @@ def test_multi_disabled_and_single_model(pkg, monkeypatch):
                          [torch.zeros(2, dtype=torch.int64, device=det.device)])
     assert [x.cpu().tolist() for x in a] == [x.cpu().tolist() for x in b]
     assert c[0].cpu().tolist() == a[0].cpu().tolist()
+
+
+def test_multi_runs_persistent_batches_alone(pkg, monkeypatch):
+    """A model whose batch is past the persistent launch's capacity (cvd_model_info.
+    persist_seqs; capped at 2 blocks here so that small batches cross it) is launched alone
+    and persistently, the rest merged; sums and counts equal the all-merged block launch, and
+    multi_groups (bench.py's per-launch timing) gives the same split."""
+    ps = [0.02, 0.05, 0.1, 0.2]
+    T = [1500, 300, 2100, 700]
+    N = 2001
+    cc, det, models, bufs = _setup(pkg, ps, N, T)
+    nseq = [2 * t for t in T]
+
+    def run():
+        sums = [torch.full((2 * t, 2), float("nan"), dtype=torch.float64, device=det.device) for t in T]
+        cnts = [torch.zeros(2, dtype=torch.int64, device=det.device) for _ in T]
+        det.detect_multi(models, bufs, N, nseq, T, cnts, sums=sums)
+        return [s.cpu().numpy() for s in sums], [c.cpu().tolist() for c in cnts]
+
+    monkeypatch.setenv("CVD_K1S_PERSIST", "0")
+    assert all(m.info()["persist_seqs"] == 0 for m in models)
+    assert det.multi_groups(models, nseq) == [[0, 1, 2, 3]]
+    ref_s, ref_c = run()
+    monkeypatch.setenv("CVD_K1S_PERSIST", "1")
+    monkeypatch.setenv("CVD_K1S_PERSIST_BLOCKS", "2")
+    cap = models[0].info()["persist_seqs"]
+    assert cap == 2 * 1024
+    alone = [i for i, s in enumerate(nseq) if s > cap]
+    assert alone == [0, 2]
+    assert det.multi_groups(models, nseq) == [[0], [1], [2], [3]]
+    got_s, got_c = run()
+    for i in range(len(ps)):
+        assert not np.isnan(got_s[i]).any()
+        assert np.array_equal(got_s[i], ref_s[i]), ps[i]
+    assert got_c == ref_c
