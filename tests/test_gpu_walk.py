@@ -197,3 +197,21 @@ def test_persistent_launch_equals_block_launch(pkg, monkeypatch, p, walk):
         assert np.array_equal(got, ref), (p, N)
         assert gc == rc
     assert model.device_error() == 0
+
+
+@pytest.mark.parametrize("p,walk", [(0.01, "1"), (0.1, "0")])
+def test_persistent_launch_early_decision_counts(pkg, monkeypatch, p, walk):
+    """Counts-only early decision under the work-queue launch (a wave that has decided its
+    64 trials takes the next unit): the block launch's counts, which equal the full run's."""
+    cc, det = _m6(pkg)
+    model = det.model(p, 200_000, 200, 1.0, SEED)
+    monkeypatch.setenv("CVD_WALK", walk)
+    args = (model, cc["gen1"], cc["gen2"], 20_000, p, SEED, 3, 3 + 2500)
+    monkeypatch.setenv("CVD_K1S_PERSIST", "0")
+    full = det.run_trials(*args)["counts"].cpu().tolist()
+    block = det.run_trials(*args, early_decision=True)["counts"].cpu().tolist()
+    monkeypatch.setenv("CVD_K1S_PERSIST", "1")
+    monkeypatch.setenv("CVD_K1S_PERSIST_BLOCKS", "2")
+    pers = det.run_trials(*args, early_decision=True)["counts"].cpu().tolist()
+    assert pers == block == full
+    assert model.device_error() == 0
