@@ -217,7 +217,11 @@ int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int
  * q < n_h1 are H1 streams (success iff logp1 > logref), the rest H2 streams
  * (success iff logp1 <= logref) (Pd_plotter.py:215-223).  d_counts[0] += H1
  * successes, d_counts[1] += H2 successes (int64, accumulated, not cleared).
- * d_sums (nullable): [nseq][2] doubles. */
+ * d_sums (nullable): [nseq][2] doubles.
+ * A launch of the bit-sliced kernel past cvd_model_info.persist_seqs is persistent: its
+ * waves take their sequences from a work-queue counter, one of a ring of 64 per model that
+ * the call zeroes on `stream`; at most 64 such launches of one model may be in flight at
+ * once (across streams). */
 int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
                int64_t n_h1, double* d_sums, int64_t* d_counts, int32_t path, void* stream);
 
