@@ -205,3 +205,27 @@ def test_explicit_grid_batch_is_clamped_to_the_budget(pkg):
     b = clamp_grid_batch(models, g1, N_list, 1000, 0, row // 2)
     assert 1 <= b < 1000 and grid_workspace_bytes(models, g1, N_list, b, 0) <= row // 2
     assert clamp_grid_batch(models, g1, N_list, 1000, 0, row) == 1000
+
+
+def test_multi_groups_follow_variant_and_persistence(pkg, monkeypatch):
+    """Detector.multi_groups (bench.py's per-launch timing) mirrors cvd_detect_multi's merge
+    rule: runs of one nonzero variant, at most 8, a model whose batch is past its
+    persist_seqs alone (ABI 10), CVD_NO_MULTI=1 every model alone."""
+    class M:
+        def __init__(self, v, cap):
+            self.inf = {"multi_variant": v, "persist_seqs": cap}
+
+        def info(self):
+            return self.inf
+
+    monkeypatch.delenv("CVD_NO_MULTI", raising=False)
+    g = pkg.Detector.multi_groups
+    ms = [M(7, 0), M(7, 0), M(9, 0), M(9, 0), M(0, 0), M(9, 0)]
+    assert g(ms) == [[0, 1], [2, 3], [4], [5]]
+    assert g([M(7, 0)] * 10) == [list(range(8)), [8, 9]]
+    cap = [M(7, 1000)] * 4
+    assert g(cap, [500, 500, 500, 500]) == [[0, 1, 2, 3]]
+    assert g(cap, [500, 2000, 500, 500]) == [[0], [1], [2, 3]]
+    assert g(cap) == [[0, 1, 2, 3]]          # no batch sizes: variant only
+    monkeypatch.setenv("CVD_NO_MULTI", "1")
+    assert g(ms[:2]) == [[0], [1]]
