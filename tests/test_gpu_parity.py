@@ -393,3 +393,28 @@ def test_m6_batch_beyond_32bit_offsets(pkg, dev):
     c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
     _, want = C.Model(c1, p, 200_000, 200, 1.0, seed).run_trials(c1, c2, N, p, seed, B - 2, B, sums=True)
     assert np.array_equal(s[:2], want[:, :2]) and np.array_equal(s[2:], want[:, 2:])
+
+
+@pytest.mark.parametrize("walk", ["0", "1"])
+def test_m6_bitslice_small_and_ragged_N_vs_c_oracle(pkg, dev, monkeypatch, walk):
+    """The bit-sliced kernel's step loop runs six steps per iteration (one per layout phase)
+    and then the last 1-5; its stream chunks are four words (64 steps).  Every N around
+    those boundaries -- and N = 0, 1 -- gives the C oracle's per-trial sums, lockstep and in
+    walk mode, on a persistent launch (2 blocks) and a block launch."""
+    from oracle import c_oracle as C
+    cc = pkg.CONFIG_CODES["m6"]
+    det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
+    p = 0.02
+    model = det.model(p, 100_000, 200, 1.0, 12345)
+    c1, c2 = C.Code(cc["gen1"], 6, 1, 2), C.Code(cc["gen2"], 6, 1, 2)
+    cm = C.Model(c1, p, 100_000, 200, 1.0, 12345)
+    monkeypatch.setenv("CVD_WALK", walk)
+    for N in (0, 1, 5, 6, 7, 11, 12, 13, 15, 16, 17, 63, 64, 65, 127, 129):
+        want_c, want = cm.run_trials(c1, c2, N, p, 12345, 40, 40 + 2100, sums=True, nthreads=8)
+        for persist in ("0", "1"):
+            monkeypatch.setenv("CVD_K1S_PERSIST", persist)
+            monkeypatch.setenv("CVD_K1S_PERSIST_BLOCKS", "2")
+            got = det.run_trials(model, cc["gen1"], cc["gen2"], N, p, 12345, 40, 40 + 2100, return_sums=True)
+            assert np.array_equal(got["sums"], want), (N, persist)
+            assert tuple(got["counts"].cpu().tolist()) == tuple(int(x) for x in want_c), (N, persist)
+    assert model.device_error() == 0
