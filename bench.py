@@ -535,12 +535,14 @@ def main():
             cpi = pmc.get("valu_cycles_per_inst")
             valu = {"insts_per_wave_step": ipws, "achieved": ach, "peak": VALU_PEAK_WINST,
                     "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WINST,
-                    # the same instructions priced at their measured issue cost (VOP3/VOP3P ~4.2-4.5
-                    # cycles, VOP2 ~2.6, profiles/valu_issue_cycles.json) instead of 2 cycles each
+                    # the same instructions priced at their measured issue cost per opcode and
+                    # operand kind (~2.4-2.8 cycles for bitop3 / logic / add / lshr with vector or
+                    # constant sources, ~4.2-4.6 with a scalar source and for the other opcodes;
+                    # profiles/valu_issue_cycles_r05.json) instead of 2 cycles each
                     "cycles_per_inst": cpi,
                     "issue_cycle_weighted_frac": (ach * cpi / (1024 * SHADER_GHZ * 1e9)) if cpi else None,
-                    "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU, opcode mix x "
-                              "profiles/valu_issue_cycles.json) + live HIP-event time of the launch"}
+                    "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU, instruction mix x "
+                              "profiles/valu_issue_cycles_r05.json) + live HIP-event time of the launch"}
     c = counts.cpu().numpy()
     per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, steps_at[i] * B * world),
                       "Pc": float(c[i, 0] + c[i, 1]) / max(1, 2 * steps_at[i] * B * world),

@@ -94,6 +94,7 @@ constexpr unsigned kTtAndX = 0x60;     // a & (b ^ c)
 constexpr unsigned kTtNorX = 0x09;     // ~(a | (b ^ c))
 constexpr unsigned kTtXorOr = 0xBE;    // (a ^ b) | c
 constexpr unsigned kTtNor3 = 0x01;     // ~(a | b | c)
+constexpr unsigned kTtOr3 = 0xFE;      // a | b | c
 constexpr unsigned kTtAndXor = 0x28;   // (a ^ b) & c   (not used by the kernel; tests)
 constexpr unsigned kTtSel = 0xCA;      // a ? b : c, bitwise (v_bfi_b32)
 constexpr unsigned kTtAndNotOr = 0xBA; // (a & ~b) | c
@@ -113,6 +114,44 @@ CVD_HD bs_u32 bs_perm(bs_u32 hi, bs_u32 lo, bs_u32 sel) {
   return out;
 #endif
 }
+// Operand forms for gfx950's VALU issue (profiles/r05an/vib2-3.json, 4 waves per SIMD):
+// v_bitop3 / and / or / xor / add / lshrrev with VGPR, inline or literal operands issue at
+// ~2.5-2.8 cycles per wave64 instruction, the same with an SGPR (or SGPR-pair / VCC) source
+// at ~4.2, and v_lshlrev, v_or3, v_bfi, v_perm, v_cndmask at ~4.2 whatever the operands.  So
+// (CVD_BS_VFAST, default on) a bitop3 mask constant is moved into a VGPR once per use site
+// group (VOP3 takes no literal here; the compiler's own choice is an SGPR), x << 1 is an add,
+// and the step's mu mask is a VGPR value (the compiler's form: v_cndmask on VCC).
+#ifndef CVD_BS_VFAST
+#define CVD_BS_VFAST 1
+#endif
+template <bs_u32 C>
+CVD_HD bs_u32 bs_vconst() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CVD_BS_VFAST != 0) {
+    bs_u32 c;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(c) : "i"(C));
+    return c;
+  }
+#endif
+  return C;
+}
+CVD_HD bs_u32 bs_vreg(bs_u32 x) {   // an opaque VGPR copy (no SGPR / VCC-select forms of its uses)
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CVD_BS_VFAST != 0) asm volatile("" : "+v"(x));
+#endif
+  return x;
+}
+template <int S>
+CVD_HD bs_u32 bs_shl(bs_u32 x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CVD_BS_VFAST != 0 && S == 1) {
+    bs_u32 r;
+    asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+  }
+#endif
+  return x << S;
+}
 CVD_HD bs_u32 bs_rot16(bs_u32 x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_alignbit(x, x, 16u);
@@ -122,16 +161,19 @@ CVD_HD bs_u32 bs_rot16(bs_u32 x) {
 }
 
 // positions p <-> p ^ (1 << K) within a word (the partner flip of a location 0..4)
+// (K < 3: the lower position of each pair, m = bs_flip_mask<K>, as an operand so that a caller
+// flipping several planes moves it into a VGPR once)
 template <int K>
-CVD_HD bs_u32 bs_flip(bs_u32 x) {
+constexpr bs_u32 bs_flip_mask() { return K == 0 ? 0x55555555u : K == 1 ? 0x33333333u : 0x0F0F0F0Fu; }
+template <int K>
+CVD_HD bs_u32 bs_flip(bs_u32 x, bs_u32 m = bs_flip_mask<K < 3 ? K : 0>()) {
   if constexpr (K == 4) {
     return bs_rot16(x);
   } else if constexpr (K == 3) {
     return bs_perm(x, x, 0x02030001u);   // bytes 0 <-> 1, 2 <-> 3
   } else {
     constexpr int S = 1 << K;
-    constexpr bs_u32 m = K == 0 ? 0x55555555u : K == 1 ? 0x33333333u : 0x0F0F0F0Fu;
-    return bs_bop3<kTtSel>(m, x >> S, x << S);
+    return bs_bop3<kTtSel>(m, x >> S, bs_shl<S>(x));
   }
 }
 
@@ -144,8 +186,9 @@ CVD_HD bs_u32 bs_flip(bs_u32 x) {
 template <int I>
 CVD_HD void bs_swapR(bs_u32& lo, bs_u32& hi) {
   constexpr int D = 1 << I;
-  constexpr bs_u32 m1 = I == 0 ? 0xAAAAAAAAu : I == 1 ? 0xCCCCCCCCu : 0xF0F0F0F0u;   // bit I of the position set
-  const bs_u32 l2 = bs_bop3<kTtSel>(m1, hi << D, lo);
+  constexpr bs_u32 m1c = I == 0 ? 0xAAAAAAAAu : I == 1 ? 0xCCCCCCCCu : 0xF0F0F0F0u;   // bit I of the position set
+  const bs_u32 m1 = bs_vconst<m1c>();
+  const bs_u32 l2 = bs_bop3<kTtSel>(m1, bs_shl<D>(hi), lo);
   const bs_u32 h2 = bs_bop3<kTtSel>(m1, hi, lo >> D);
   lo = l2;
   hi = h2;
@@ -262,13 +305,14 @@ CVD_HD void bs_min(const bs_u32 (&a)[4], const bs_u32 (&b)[4], bs_u32 (&o)[4]) {
 template <int PH>
 CVD_HD void bs_partner(const bs_u32 (&R)[2][4], bs_u32 (&P)[2][4]) {
   constexpr int L5 = bs_sigma(PH, 5);
+  const bs_u32 m = L5 < 3 ? bs_vconst<bs_flip_mask<L5 < 3 ? L5 : 0>()>() : 0u;
   for (int i = 0; i < 4; ++i) {
     if constexpr (L5 == 5) {
       P[0][i] = R[1][i];
       P[1][i] = R[0][i];
     } else {
-      P[0][i] = bs_flip<L5>(R[0][i]);
-      P[1][i] = bs_flip<L5>(R[1][i]);
+      P[0][i] = bs_flip<L5>(R[0][i], m);
+      P[1][i] = bs_flip<L5>(R[1][i], m);
     }
   }
 }
@@ -297,12 +341,12 @@ CVD_HD void bs_step_core(const bs_u32 (&R)[2][4], const bs_u32 (&e0)[2], const b
   // mu first: a zero state with e even
   bs_u32 z[2];
   for (int r = 0; r < 2; ++r) {
-    const bs_u32 t = R[r][0] | R[r][1] | R[r][2];
+    const bs_u32 t = bs_bop3<kTtOr3>(R[r][0], R[r][1], R[r][2]);
     z[r] = bs_bop3<kTtNor3>(t, R[r][3], e0[r]);
   }
   const bool zero_hit = (z[0] | z[1]) != 0u;
   mu = zero_hit ? 0u : 1u;
-  const bs_u32 M = zero_hit ? 0u : ~0u;
+  const bs_u32 M = bs_vreg(zero_hit ? 0u : ~0u);
   bs_u32 P[2][4];
   bs_partner<PH>(R, P);
   bs_u32 dh[2] = {0u, 0u};

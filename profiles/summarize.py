@@ -171,12 +171,13 @@ def main(src, name):
         for _name, ins in isa_breakdown.blocks(isa_breakdown.main_loop(lines, 1 if bs else 0)):
             for x in ins:
                 if x.startswith("v_"):
-                    mix[x.split()[0]] = mix.get(x.split()[0], 0) + (1 / 6 if bs else 0.25)
-        cyc, by = valu_model.load_cycles()
-        avg, by_class = valu_model.weighted_cycles(mix, cyc)
+                    mix[x.strip()] = mix.get(x.strip(), 0) + (1 / 6 if bs else 0.25)
+        # round 5: priced per instruction line, operands included (valu_model.line_cycles_r05)
+        avg, by_class = valu_model.weighted_line_cycles(mix)
         out["valu_cycles_per_inst"] = avg
-        out["valu_cycles_source"] = ("static opcode mix of the step loop (profiles/isa_breakdown.py) x measured "
-                                     "issue cost per class (profiles/valu_issue_cycles.json)")
+        out["valu_cycles_source"] = ("static instruction mix of the step loop (profiles/isa_breakdown.py) x measured "
+                                     "issue cost per opcode and operand kind (profiles/valu_issue_cycles_r05.json, "
+                                     "profiles/r05an)")
         out["valu_mix_by_class_per_step"] = by_class
         out["valu_issue_cycle_frac"] = per.get("SQ_INSTS_VALU", 0.0) * avg / (1024 * max(1.0, kernel_cycles))
         for e in out["per_p"].values():

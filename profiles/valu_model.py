@@ -57,6 +57,55 @@ def load_cycles(path=None):
     return {r["op"]: r["cycles_per_wave_inst_per_simd"] for r in d["results"]}, d
 
 
+import re
+
+# ─── round 5: operand-aware prices (profiles/valu_issue_cycles_r05.json, from profiles/r05an) ───
+# On gfx950 the issue cost depends on the operands as much as on the opcode: bitop3, and, or,
+# xor, not, mov, add, sub and lshrrev issue at ~2.4-2.8 cycles per wave64 instruction with
+# VGPR, inline-constant or literal sources and at ~4.1-4.4 with any SGPR (or SGPR-pair / VCC)
+# source; lshlrev, bfi, perm, alignbit, bfe, add3, or3, and_or, lshl_or, min, med3, mul*, mad,
+# 64-bit shifts, packed and f64 ops and cndmask issue at ~4.2-4.6 whatever their operands.
+# (The class table above priced every VOP3 op, bitop3 included, at its SGPR-operand cost.)
+FAST_R05 = {"v_bitop3_b32": 2.70, "v_and_b32": 2.57, "v_or_b32": 2.54, "v_xor_b32": 2.60, "v_not_b32": 2.43,
+            "v_mov_b32": 2.39, "v_add_u32": 2.50, "v_sub_u32": 2.49, "v_subrev_u32": 2.49, "v_lshrrev_b32": 2.41}
+SLOW_R05 = {"v_add_f64": 4.57, "v_mul_f64": 4.57, "v_add3_u32": 4.64, "v_mad_u64_u32": 4.43, "v_lshl_add_u64": 4.43,
+            "v_mul_lo_u32": 4.41}
+SLOW_DEFAULT_R05 = 4.25      # every other opcode, and a fast opcode with a scalar source
+_SREG = re.compile(r"(?<![\w\[])(s\d+|s\[\d+:\d+\]|vcc|exec|m0)(?!\w)")
+
+
+def line_cycles_r05(line):
+    """(class, cycles) of one VALU instruction line of the ISA (operand-aware)."""
+    parts = line.split(None, 1)
+    op = re.sub(r"_e(32|64)$", "", parts[0])
+    operands = re.sub(r"bitop3:\S+|op_sel\S*|clamp|offset:\S+", "", parts[1] if len(parts) > 1 else "")
+    fields = [f.strip() for f in operands.split(",")]
+    # sources: everything after the destination(s) (v_cmp*: the SGPR-pair / VCC destination;
+    # v_mad_u64_u32: the carry-out SGPR pair after the vector destination)
+    nd = 2 if op in ("v_mad_u64_u32", "v_mad_i64_i32") else 1
+    srcs = ",".join(fields[nd:])
+    scalar = bool(_SREG.search(srcs))
+    if op in FAST_R05:
+        return (op + (" (scalar src)" if scalar else ""), SLOW_DEFAULT_R05 if scalar else FAST_R05[op])
+    return (op, SLOW_R05.get(op, SLOW_DEFAULT_R05))
+
+
+def weighted_line_cycles(lines_per_step):
+    """(average issue cycles per VALU instruction, per-class breakdown) of a mix of ISA lines
+    (line -> instructions per step), priced by line_cycles_r05."""
+    tot_n, tot_c, by = 0.0, 0.0, {}
+    for line, n in lines_per_step.items():
+        if not line.startswith("v_"):
+            continue
+        cls, cyc = line_cycles_r05(line)
+        tot_n += n
+        tot_c += n * cyc
+        b = by.setdefault(cls, [0.0, 0.0])
+        b[0] += n
+        b[1] += n * cyc
+    return tot_c / max(tot_n, 1e-9), {k: {"insts_per_step": v[0], "cycles_per_step": v[1]} for k, v in by.items()}
+
+
 def weighted_cycles(opcodes_per_step, cycles):
     """(average issue cycles per VALU instruction, per-class breakdown) of a mix."""
     tot_n, tot_c, by = 0.0, 0.0, {}
