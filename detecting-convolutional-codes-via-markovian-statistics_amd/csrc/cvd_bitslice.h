@@ -121,13 +121,14 @@ CVD_HD bs_u32 bs_perm(bs_u32 hi, bs_u32 lo, bs_u32 sel) {
 // (CVD_BS_VFAST, default on) a bitop3 mask constant is moved into a VGPR once per use site
 // group (VOP3 takes no literal here; the compiler's own choice is an SGPR), x << 1 is an add,
 // and the step's mu mask is a VGPR value (the compiler's form: v_cndmask on VCC).
+// (bits, for A/Bs: 1 the masks, 2 the add, 4 the mu mask, 8 the zero test's OR as a bitop3)
 #ifndef CVD_BS_VFAST
-#define CVD_BS_VFAST 1
+#define CVD_BS_VFAST 15
 #endif
 template <bs_u32 C>
 CVD_HD bs_u32 bs_vconst() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CVD_BS_VFAST != 0) {
+  if constexpr ((CVD_BS_VFAST & 1) != 0) {
     bs_u32 c;
     asm volatile("v_mov_b32 %0, %1" : "=v"(c) : "i"(C));
     return c;
@@ -137,14 +138,14 @@ CVD_HD bs_u32 bs_vconst() {
 }
 CVD_HD bs_u32 bs_vreg(bs_u32 x) {   // an opaque VGPR copy (no SGPR / VCC-select forms of its uses)
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CVD_BS_VFAST != 0) asm volatile("" : "+v"(x));
+  if constexpr ((CVD_BS_VFAST & 4) != 0) asm volatile("" : "+v"(x));
 #endif
   return x;
 }
 template <int S>
 CVD_HD bs_u32 bs_shl(bs_u32 x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CVD_BS_VFAST != 0 && S == 1) {
+  if constexpr ((CVD_BS_VFAST & 2) != 0 && S == 1) {
     bs_u32 r;
     asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
     return r;
@@ -341,7 +342,7 @@ CVD_HD void bs_step_core(const bs_u32 (&R)[2][4], const bs_u32 (&e0)[2], const b
   // mu first: a zero state with e even
   bs_u32 z[2];
   for (int r = 0; r < 2; ++r) {
-    const bs_u32 t = bs_bop3<kTtOr3>(R[r][0], R[r][1], R[r][2]);
+    const bs_u32 t = (CVD_BS_VFAST & 8) ? bs_bop3<kTtOr3>(R[r][0], R[r][1], R[r][2]) : R[r][0] | R[r][1] | R[r][2];
     z[r] = bs_bop3<kTtNor3>(t, R[r][3], e0[r]);
   }
   const bool zero_hit = (z[0] | z[1]) != 0u;
