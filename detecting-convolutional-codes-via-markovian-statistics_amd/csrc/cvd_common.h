@@ -104,6 +104,58 @@ CVD_HD void philox_blocks(uint32_t (&c)[B][4], uint32_t k0, uint32_t k1) {
   }
 }
 
+// The ten round keys (k0 + r W0, k1 + r W1) of a Philox key held in VGPRs: a v_bitop3 with a
+// scalar source issues at ~4.3 cycles per wave64 instruction on gfx950, with vector sources at
+// ~2.8 (profiles/r05an), and the compiler re-copies a uniform key into a VGPR at every use
+// rather than hoist it -- so a caller that runs many blocks under one key precomputes them
+struct PhiloxKeysV {
+  uint32_t k[20];
+  CVD_HD void init(uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      k[2 * r] = k0 + (uint32_t)r * kPhiloxW0;
+      k[2 * r + 1] = k1 + (uint32_t)r * kPhiloxW1;
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int i = 0; i < 20; ++i) asm volatile("" : "+v"(k[i]));
+#endif
+  }
+};
+template <int B>
+CVD_HD void philox_blocks(uint32_t (&c)[B][4], const PhiloxKeysV& kv) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0[B], p1[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      p0[b] = (uint64_t)kPhiloxM0 * c[b][0];
+      p1[b] = (uint64_t)kPhiloxM1 * c[b][2];
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const uint32_t hi0 = (uint32_t)(p0[b] >> 32), lo0 = (uint32_t)p0[b];
+      const uint32_t hi1 = (uint32_t)(p1[b] >> 32), lo1 = (uint32_t)p1[b];
+#if defined(__HIP_DEVICE_COMPILE__)
+      uint32_t n0, n2;
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c[b][1]), "v"(kv.k[2 * r]));
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c[b][3]), "v"(kv.k[2 * r + 1]));
+#else
+      const uint32_t n0 = hi1 ^ c[b][1] ^ kv.k[2 * r], n2 = hi0 ^ c[b][3] ^ kv.k[2 * r + 1];
+#endif
+      c[b][0] = n0; c[b][1] = lo1; c[b][2] = n2; c[b][3] = lo0;
+    }
+  }
+}
+// the launch's key pair (SGPRs; the round keys by scalar adds per call)
+struct PhiloxKeysS {
+  uint32_t k0, k1;
+};
+template <int B>
+CVD_HD void philox_blocks(uint32_t (&c)[B][4], const PhiloxKeysS& ks) {
+  philox_blocks<B>(c, ks.k0, ks.k1);
+}
+
 CVD_HD uint32_t u4_get(const U4& v, uint32_t i) {
   return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
 }

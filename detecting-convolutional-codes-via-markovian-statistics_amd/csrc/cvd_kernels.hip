@@ -50,6 +50,10 @@ namespace {
 #endif
 // noise straggler exchange: one block per slot lane, a pair's two blocks on two lanes
 // (1), or both blocks of a pair on one slot lane (0)
+// gen_fast_kernel: the noise Philox keys' round keys precomputed in VGPRs (PhiloxKeysV)
+#ifndef CVD_GEN_VKEYS
+#define CVD_GEN_VKEYS 1
+#endif
 #ifndef CVD_GEN_XCHG_SPLIT
 #define CVD_GEN_XCHG_SPLIT 1
 #endif
@@ -283,19 +287,19 @@ __device__ __forceinline__ void noise_head_planes(const GenArgs& a, const uint32
 // Planes 1-8 (Philox blocks 0 and 1, unconditional) of word w of the sequence whose
 // counter words are `own`: U = still undecided bits, F = flips so far (straight-line
 // VALU, so a caller can interleave it with other work)
+template <class KS>
 __device__ __forceinline__ void noise_head(const GenArgs& a, uint2 own, uint32_t w, bool live, uint32_t valid,
-                                           uint32_t& U, uint32_t& F) {
+                                           uint32_t& U, uint32_t& F, const KS& ks) {
   const uint32_t t = a.thr_lo;
   U = live ? valid : 0u;
   F = 0u;
-  const uint32_t k0 = a.k0, k1 = a.k1;
   uint32_t xv[2][4];
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     xv[b][0] = w * kNoiseBlocksPerWord + (uint32_t)b;
     xv[b][1] = own.x; xv[b][2] = own.y; xv[b][3] = a.tag;
   }
-  philox_blocks<2>(xv, k0, k1);
+  philox_blocks<2>(xv, ks);
   noise_planes4(t >> 28, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U, F);
   noise_planes4(t >> 24, xv[1][0], xv[1][1], xv[1][2], xv[1][3], U, F);
 }
@@ -306,9 +310,9 @@ __device__ __forceinline__ void noise_head(const GenArgs& a, uint2 own, uint32_t
 // (8 planes) of the i-th pair and the result goes back to the owner.  seq(l): the
 // (counter word 1, counter word 2) = (seq_lo, ctr_hi(seq, noise)) of lane l's sequence,
 // for the slot lanes.
-template <typename Seq>
+template <typename Seq, class KS>
 __device__ __forceinline__ void noise_exchange_pair(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq,
-                                                    uint32_t w4, uint32_t (&U)[4], uint32_t (&F)[4]) {
+                                                    uint32_t w4, uint32_t (&U)[4], uint32_t (&F)[4], const KS& ks) {
   const uint32_t t = a.thr_lo, lane = lane_id();
   const uint32_t nslots = a.slots - 1u < 64u ? a.slots : 64u;   // 1..64: every round makes progress
 #pragma nounroll
@@ -331,7 +335,6 @@ __device__ __forceinline__ void noise_exchange_pair(const GenArgs& a, uint32_t* 
       if (busy) {
         uint32_t Un = su[lane], Fn = 0u;
         const uint32_t mm = sm[lane], src = mm & 63u, w = w4 + (mm >> 6);
-        const uint32_t k0 = a.k0, k1 = a.k1;
         const uint2 sq = seq(src);
         uint32_t xv[2][4];
 #pragma unroll
@@ -339,7 +342,7 @@ __device__ __forceinline__ void noise_exchange_pair(const GenArgs& a, uint32_t* 
           xv[b][0] = w * kNoiseBlocksPerWord + j + (uint32_t)b;
           xv[b][1] = sq.x; xv[b][2] = sq.y; xv[b][3] = a.tag;
         }
-        philox_blocks<2>(xv, k0, k1);
+        philox_blocks<2>(xv, ks);
         noise_planes4(t >> (28u - 4u * j), xv[0][0], xv[0][1], xv[0][2], xv[0][3], Un, Fn);
         noise_planes4(t >> (24u - 4u * j), xv[1][0], xv[1][1], xv[1][2], xv[1][3], Un, Fn);
         su[lane] = Un; sm[lane] = Fn;
@@ -360,9 +363,9 @@ __device__ __forceinline__ void noise_exchange_pair(const GenArgs& a, uint32_t* 
 // pairs left after planes 1-8 of four words nearly always fit one round).  Measured:
 // the generator alone 1% faster, the fused kernel (4 more VGPRs) slower
 // (profiles/r04n); so the generator uses it and the fused kernel does not.
-template <typename Seq>
+template <typename Seq, class KS>
 __device__ __forceinline__ void noise_exchange_split(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq,
-                                                     uint32_t w4, uint32_t (&U)[4], uint32_t (&F)[4]) {
+                                                     uint32_t w4, uint32_t (&U)[4], uint32_t (&F)[4], const KS& ks) {
   const uint32_t t = a.thr_lo, lane = lane_id();
   const uint32_t nslots = a.slots - 1u < 64u ? a.slots : 64u;
   const uint32_t npr = nslots > 1u ? nslots >> 1 : 1u;   // pairs per round
@@ -386,10 +389,9 @@ __device__ __forceinline__ void noise_exchange_split(const GenArgs& a, uint32_t*
       if (pi < npr && s0 + pi < tot) {
         // (the read of sm[pi] returns before this lane's writes below: they depend on it)
         const uint32_t mm = sm[pi], src = mm & 63u, w = w4 + (mm >> 6), blk = j + (lane & 1u);
-        const uint32_t k0 = a.k0, k1 = a.k1;
         const uint2 sq = seq(src);
         uint32_t xv[1][4] = {{w * kNoiseBlocksPerWord + blk, sq.x, sq.y, a.tag}};
-        philox_blocks<1>(xv, k0, k1);
+        philox_blocks<1>(xv, ks);
         uint32_t eq = ~0u, lt = 0u;
         noise_planes4<true>(t >> (28u - 4u * blk), xv[0][0], xv[0][1], xv[0][2], xv[0][3], eq, lt);
         su[lane] = lt; sm[lane] = eq;
@@ -409,11 +411,11 @@ __device__ __forceinline__ void noise_exchange_split(const GenArgs& a, uint32_t*
   }
 }
 
-template <bool kSplit, typename Seq>
+template <bool kSplit, typename Seq, class KS>
 __device__ __forceinline__ void noise_exchange(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
-                                               uint32_t (&U)[4], uint32_t (&F)[4]) {
-  if constexpr (kSplit) noise_exchange_split(a, su, sm, seq, w4, U, F);
-  else noise_exchange_pair(a, su, sm, seq, w4, U, F);
+                                               uint32_t (&U)[4], uint32_t (&F)[4], const KS& ks) {
+  if constexpr (kSplit) noise_exchange_split(a, su, sm, seq, w4, U, F, ks);
+  else noise_exchange_pair(a, su, sm, seq, w4, U, F, ks);
 }
 
 // Flip masks F[g] of the words w4 + g (g < 4) of every lane's sequence, noise_word's
@@ -426,20 +428,21 @@ __device__ __forceinline__ void noise_exchange(const GenArgs& a, uint32_t* su, u
 //    ballot finds one.
 // One word at a time (3 blocks for every lane, then single blocks while any lane is
 // undecided) costs ~3.4 blocks per word; this ~2.5.
-template <typename Seq>
+template <typename Seq, class KS>
 __device__ __forceinline__ void noise_chunk_wave(const GenArgs& a, uint32_t* su, uint32_t* sm, Seq seq, uint32_t w4,
-                                                 const bool (&live)[4], uint32_t valid, uint32_t (&F)[4]) {
+                                                 const bool (&live)[4], uint32_t valid, uint32_t (&F)[4], const KS& ks) {
   uint32_t U[4];
   const uint2 own = seq(lane_id());
 #pragma unroll
-  for (int g = 0; g < 4; ++g) noise_head(a, own, w4 + g, live[g], valid, U[g], F[g]);
-  noise_exchange<CVD_GEN_XCHG_SPLIT>(a, su, sm, seq, w4, U, F);
+  for (int g = 0; g < 4; ++g) noise_head(a, own, w4 + g, live[g], valid, U[g], F[g], ks);
+  noise_exchange<CVD_GEN_XCHG_SPLIT>(a, su, sm, seq, w4, U, F, ks);
 }
 
 // Encoder of one sequence, one received word at a time (bit-parallel, see above):
 // the input stream's Philox block cache and the window history carried from word
 // to word.  encode(w, nm) returns word w with the flip mask nm applied.
-template <int k, int n, int kT = 0>
+// kVK: the noise keys' ten round keys in VGPRs (PhiloxKeysV; gen_fast_kernel, CVD_GEN_VKEYS)
+template <int k, int n, int kT = 0, bool kVK = false>
 struct ChunkEncoder {
   static constexpr int SPW = 32 / n, NBITS = SPW * n;
   static constexpr uint32_t kValid = NBITS == 32 ? ~0u : (1u << (NBITS % 32)) - 1u;
@@ -475,8 +478,16 @@ struct ChunkEncoder {
   int64_t iblk;
   U4 iv;
   uint32_t sprev[k], hist[k];
+  struct NoKeys {};
+  typename std::conditional<kVK, PhiloxKeysV, NoKeys>::type kv;
+  // the noise blocks' key: the launch's pair (SGPRs), or the VGPR round keys
+  __device__ __forceinline__ auto keys() const {
+    if constexpr (kVK) return kv;
+    else return PhiloxKeysS{a->k0, a->k1};
+  }
   __device__ void init(const GenArgs* a_, uint64_t sid) {
     a = a_;
+    if constexpr (kVK) kv.init(a->k0, a->k1);
     slo = (uint32_t)sid; ihi = ctr_hi(sid, kKindInput);
     iblk = -1; iv = U4{0u, 0u, 0u, 0u};
 #pragma unroll
@@ -485,9 +496,15 @@ struct ChunkEncoder {
   __device__ uint32_t input_word(int64_t W) {   // 32-bit word W of the input stream
     if ((W >> 2) != iblk) {
       iblk = W >> 2;
-      uint32_t k0 = a->k0, k1 = a->k1;
-      asm volatile("" : "+s"(k0), "+s"(k1));
-      iv = philox((uint32_t)iblk, slo, ihi, a->tag, k0, k1);
+      if constexpr (kVK) {
+        uint32_t c[1][4] = {{(uint32_t)iblk, slo, ihi, a->tag}};
+        philox_blocks<1>(c, kv);
+        iv = U4{c[0][0], c[0][1], c[0][2], c[0][3]};
+      } else {
+        uint32_t k0 = a->k0, k1 = a->k1;
+        asm volatile("" : "+s"(k0), "+s"(k1));
+        iv = philox((uint32_t)iblk, slo, ihi, a->tag, k0, k1);
+      }
     }
     return u4_get(iv, (uint32_t)(W & 3));
   }
@@ -530,11 +547,11 @@ struct ChunkEncoder {
   // hoisting the n kT extracted shifts out of the chunk loop into SGPRs (18 for rate 2/3:
   // SGPR spills to VGPR lanes); per word the words and one s_lshr per slot
   __device__ __forceinline__ void tap_words(int j, uint32_t& p0, uint32_t& p1) const {
-    p0 = a->tpk[j][0];
+    p0 = __builtin_amdgcn_readfirstlane(a->tpk[j][0]);
     asm volatile("" : "+s"(p0));
     p1 = 0u;
     if constexpr (kT > 6) {
-      p1 = a->tpk[j][1];
+      p1 = __builtin_amdgcn_readfirstlane(a->tpk[j][1]);
       asm volatile("" : "+s"(p1));
     }
   }
@@ -564,7 +581,7 @@ struct ChunkEncoder {
         for (int r = 0; r < 2; ++r) {
           // window tap sh of phase r is u_r(t - (hs - sh)): X bit 30 + 3 (t - hs + sh) + r,
           // moved to bit 3t + j (the scalar loop over the set taps, as below)
-          uint32_t tm = a->taps[j][r];
+          uint32_t tm = __builtin_amdgcn_readfirstlane(a->taps[j][r]);
           asm volatile("" : "+s"(tm));
 #pragma nounroll
           while (tm) {
@@ -617,7 +634,7 @@ struct ChunkEncoder {
         // two VALU per tap.  The mask is re-read per word -- hoisted out of
         // the chunk loop, per-shift conditions filled the SGPRs (spills) and
         // unrolled they became selects for every possible shift
-        uint32_t tm = a->taps[j][r];
+        uint32_t tm = __builtin_amdgcn_readfirstlane(a->taps[j][r]);
         asm volatile("" : "+s"(tm));
 #pragma nounroll
         while (tm) {
@@ -650,7 +667,7 @@ struct ChunkEncoder {
 #pragma unroll
       for (int g = 0; g < 4; ++g) nm4[g] = kValid;
     } else if (a->thr_lo) {
-      noise_chunk_wave(*a, su, sm, seq, (uint32_t)w4, live, kValid, nm4);
+      noise_chunk_wave(*a, su, sm, seq, (uint32_t)w4, live, kValid, nm4, keys());
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) out4[g] = w4 + g < nwords ? encode(w4 + g, nm4[g]) : 0u;
@@ -658,7 +675,7 @@ struct ChunkEncoder {
   // the same in two parts, so that a caller can interleave the unconditional noise
   // blocks with other work: head(g) for g = 0..3, then finish (wave-collective)
   __device__ void head(uint2 own, int64_t w, bool live, uint32_t& U, uint32_t& F) const {
-    noise_head(*a, own, (uint32_t)w, live, kValid, U, F);
+    noise_head(*a, own, (uint32_t)w, live, kValid, U, F, keys());
   }
   template <typename Seq>
   __device__ void finish(uint32_t* su, uint32_t* sm, Seq seq, int64_t w4, uint32_t (&U)[4], uint32_t (&F)[4],
@@ -667,7 +684,7 @@ struct ChunkEncoder {
 #pragma unroll
       for (int g = 0; g < 4; ++g) F[g] = kValid;
     } else if (a->thr_lo) {
-      noise_exchange<CVD_FUSED_XCHG_SPLIT>(*a, su, sm, seq, (uint32_t)w4, U, F);
+      noise_exchange<CVD_FUSED_XCHG_SPLIT>(*a, su, sm, seq, (uint32_t)w4, U, F, keys());
     } else {
 #pragma unroll
       for (int g = 0; g < 4; ++g) F[g] = 0u;
@@ -713,7 +730,7 @@ __global__ __launch_bounds__(kBlock) void gen_fast_kernel(GenArgs a) {
 #endif
   const int64_t nwords = (a.N + SPW - 1) / SPW;
   const int64_t nw4 = (nwords + 3) & ~(int64_t)3;
-  ChunkEncoder<k, n, kT> enc;
+  ChunkEncoder<k, n, kT, CVD_GEN_VKEYS != 0> enc;
   enc.init(&a, sid);
   // segment blockIdx.y of the sequence's 16-byte chunks: every word depends only
   // on its own inputs and the hs input steps before it, so segments are
