@@ -108,9 +108,16 @@ CVD_HD void philox_blocks(uint32_t (&c)[B][4], uint32_t k0, uint32_t k1) {
 // scalar source issues at ~4.3 cycles per wave64 instruction on gfx950, with vector sources at
 // ~2.8 (profiles/r05an), and the compiler re-copies a uniform key into a VGPR at every use
 // rather than hoist it -- so a caller that runs many blocks under one key precomputes them
+#ifndef CVD_PHILOX_VMUL
+#define CVD_PHILOX_VMUL 0
+#endif
 struct PhiloxKeysV {
   uint32_t k[20];
+  uint32_t m0 = kPhiloxM0, m1 = kPhiloxM1;   // (CVD_PHILOX_VMUL: the multipliers in VGPRs too)
   CVD_HD void init(uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (CVD_PHILOX_VMUL) asm volatile("" : "+v"(m0), "+v"(m1));
+#endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
       k[2 * r] = k0 + (uint32_t)r * kPhiloxW0;
@@ -129,8 +136,8 @@ CVD_HD void philox_blocks(uint32_t (&c)[B][4], const PhiloxKeysV& kv) {
     uint64_t p0[B], p1[B];
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-      p0[b] = (uint64_t)kPhiloxM0 * c[b][0];
-      p1[b] = (uint64_t)kPhiloxM1 * c[b][2];
+      p0[b] = (uint64_t)(CVD_PHILOX_VMUL ? kv.m0 : kPhiloxM0) * c[b][0];
+      p1[b] = (uint64_t)(CVD_PHILOX_VMUL ? kv.m1 : kPhiloxM1) * c[b][2];
     }
 #pragma unroll
     for (int b = 0; b < B; ++b) {

@@ -14,7 +14,8 @@ for r in $(seq 1 "$ROUNDS"); do
     python3 -c "
 import json
 d=json.loads(open('$OUT/bench_${name}_$r.json').read().strip().split('\n')[-1])
-print('$name', $r, round(d['value']), 'gen', round(d['diagnostic']['generator_ms_per_step'], 1), [(x['p'][0], round(x['ms'])) for x in d['diagnostic']['detector_ms_by_launch']])
+dg=d['diagnostic']
+print('$name', $r, round(d['value']), 'gen', round(dg.get('generator_ms_per_step') or 0, 1), [(x['p'][0], round(x['ms'])) for x in dg.get('detector_ms_by_launch', [])])
 " | tee -a "$OUT/summary.txt"
   done
 done
