@@ -154,6 +154,30 @@ CVD_HD void philox_blocks(uint32_t (&c)[B][4], const PhiloxKeysV& kv) {
     }
   }
 }
+// one round of B blocks under round r of VGPR round keys (the fused kernel's pipelined rounds)
+template <int B>
+CVD_HD void philox_round(uint32_t (&c)[B][4], const PhiloxKeysV& kv, int r) {
+  uint64_t p0[B], p1[B];
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    p0[b] = (uint64_t)kPhiloxM0 * c[b][0];
+    p1[b] = (uint64_t)kPhiloxM1 * c[b][2];
+  }
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const uint32_t hi0 = (uint32_t)(p0[b] >> 32), lo0 = (uint32_t)p0[b];
+    const uint32_t hi1 = (uint32_t)(p1[b] >> 32), lo1 = (uint32_t)p1[b];
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t n0, n2;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c[b][1]), "v"(kv.k[2 * r]));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c[b][3]), "v"(kv.k[2 * r + 1]));
+#else
+    const uint32_t n0 = hi1 ^ c[b][1] ^ kv.k[2 * r], n2 = hi0 ^ c[b][3] ^ kv.k[2 * r + 1];
+#endif
+    c[b][0] = n0; c[b][1] = lo1; c[b][2] = n2; c[b][3] = lo0;
+  }
+}
+
 // the launch's key pair (SGPRs; the round keys by scalar adds per call)
 struct PhiloxKeysS {
   uint32_t k0, k1;

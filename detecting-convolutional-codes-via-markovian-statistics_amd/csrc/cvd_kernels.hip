@@ -54,6 +54,11 @@ namespace {
 #ifndef CVD_GEN_VKEYS
 #define CVD_GEN_VKEYS 1
 #endif
+// mc_table16_kernel (the fused C1 path): the same, off by default (its 70 VGPRs hold 7 waves per
+// SIMD; the round keys cost 20)
+#ifndef CVD_FUSED_VKEYS
+#define CVD_FUSED_VKEYS 0
+#endif
 #ifndef CVD_GEN_XCHG_SPLIT
 #define CVD_GEN_XCHG_SPLIT 1
 #endif
@@ -985,7 +990,7 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
     const uint64_t sd = sid0 + 2 * (uint64_t)l;
     return make_uint2((uint32_t)sd, ctr_hi(sd, kKindNoise));
   };
-  ChunkEncoder<k, n, kT> enc;
+  ChunkEncoder<k, n, kT, CVD_FUSED_VKEYS != 0> enc;
   enc.init(&g, sid0 + 2 * (uint64_t)lane);
   const uint2 own = seq(lane);
   const int64_t N = ta.N, nwords = (N + SPW - 1) / SPW, nchunks = (nwords + 3) / 4;
@@ -1024,13 +1029,22 @@ __global__ __launch_bounds__(BS) void mc_table16_kernel(FusedArgs a) {
         }
         uint32_t k0 = g.k0, k1 = g.k1;
         uint32_t word = wv[e];
+        auto round = [&](int r) {
+          if constexpr (CVD_FUSED_VKEYS != 0) {
+            philox_round<2>(xv, enc.kv, r);
+          } else {
+            philox_round<2>(xv, k0, k1);
+            k0 += kPhiloxW0;
+            k1 += kPhiloxW1;
+          }
+        };
 #pragma unroll
         for (int i = 0; i < SPW; ++i) {
           md.step(st, __builtin_amdgcn_ubfe(word, (uint32_t)(n * i), (uint32_t)n), lp, lr);
-          if (i < 10) { philox_round<2>(xv, k0, k1); k0 += kPhiloxW0; k1 += kPhiloxW1; }
+          if (i < 10) round(i);
         }
 #pragma unroll
-        for (int r = SPW; r < 10; ++r) { philox_round<2>(xv, k0, k1); k0 += kPhiloxW0; k1 += kPhiloxW1; }
+        for (int r = SPW; r < 10; ++r) round(r);
         noise_head_planes(g, xv, valid && wn + e < nwords, ChunkEncoder<k, n, kT>::kValid, U[e], F[e]);
       }
     } else {
