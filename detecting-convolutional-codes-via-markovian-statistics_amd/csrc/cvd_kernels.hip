@@ -279,6 +279,35 @@ __device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMI
 //    from the lane index in the fused kernel).
 // One word at a time (3 blocks for every lane, then single blocks while any lane is
 // undecided) costs ~3.4 blocks per word; this ~2.5.
+// (CVD_GEN_VTHR, timing study, off: the head's eight plane masks of the threshold, 0 or ~0,
+// in VGPRs as well as the round keys -- 8 more VGPRs)
+#ifndef CVD_GEN_VTHR
+#define CVD_GEN_VTHR 0
+#endif
+struct NoiseKeysV : PhiloxKeysV {
+  uint32_t tm[8];
+  __device__ void init_thr(uint32_t t) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      tm[i] = 0u - ((t >> (31 - i)) & 1u);
+      asm volatile("" : "+v"(tm[i]));
+    }
+  }
+};
+// four planes against VGPR plane masks m[0..3] (most significant first; noise_planes4's chains)
+__device__ __forceinline__ void noise_planes4_m(const uint32_t* m, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
+                                                uint32_t& U, uint32_t& F) {
+  const uint32_t r[4] = {r0, r1, r2, r3};
+  uint32_t lt = 0u, eq = U;
+#pragma unroll
+  for (int i = 3; i >= 0; --i) {
+    asm("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x8e" : "+v"(lt) : "v"(r[i]), "v"(m[i]));
+    asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x90" : "+v"(eq) : "v"(r[i]), "v"(m[i]));
+  }
+  F |= U & lt;
+  U = eq;
+}
+
 // noise_head's plane tests on its two Philox blocks (already computed)
 __device__ __forceinline__ void noise_head_planes(const GenArgs& a, const uint32_t (&xv)[2][4], bool live,
                                                   uint32_t valid, uint32_t& U, uint32_t& F) {
@@ -305,8 +334,13 @@ __device__ __forceinline__ void noise_head(const GenArgs& a, uint2 own, uint32_t
     xv[b][1] = own.x; xv[b][2] = own.y; xv[b][3] = a.tag;
   }
   philox_blocks<2>(xv, ks);
-  noise_planes4(t >> 28, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U, F);
-  noise_planes4(t >> 24, xv[1][0], xv[1][1], xv[1][2], xv[1][3], U, F);
+  if constexpr (std::is_same<KS, NoiseKeysV>::value) {
+    noise_planes4_m(ks.tm, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U, F);
+    noise_planes4_m(ks.tm + 4, xv[1][0], xv[1][1], xv[1][2], xv[1][3], U, F);
+  } else {
+    noise_planes4(t >> 28, xv[0][0], xv[0][1], xv[0][2], xv[0][3], U, F);
+    noise_planes4(t >> 24, xv[1][0], xv[1][1], xv[1][2], xv[1][3], U, F);
+  }
 }
 
 // The straggler exchange after the heads of words w4 .. w4 + 3 (wave-collective):
@@ -484,7 +518,8 @@ struct ChunkEncoder {
   U4 iv;
   uint32_t sprev[k], hist[k];
   struct NoKeys {};
-  typename std::conditional<kVK, PhiloxKeysV, NoKeys>::type kv;
+  typename std::conditional<kVK, typename std::conditional<CVD_GEN_VTHR != 0, NoiseKeysV, PhiloxKeysV>::type,
+                            NoKeys>::type kv;
   // the noise blocks' key: the launch's pair (SGPRs), or the VGPR round keys
   __device__ __forceinline__ auto keys() const {
     if constexpr (kVK) return kv;
@@ -492,7 +527,10 @@ struct ChunkEncoder {
   }
   __device__ void init(const GenArgs* a_, uint64_t sid) {
     a = a_;
-    if constexpr (kVK) kv.init(a->k0, a->k1);
+    if constexpr (kVK) {
+      kv.init(a->k0, a->k1);
+      if constexpr (CVD_GEN_VTHR != 0) kv.init_thr(a->thr_lo);
+    }
     slo = (uint32_t)sid; ihi = ctr_hi(sid, kKindInput);
     iblk = -1; iv = U4{0u, 0u, 0u, 0u};
 #pragma unroll
