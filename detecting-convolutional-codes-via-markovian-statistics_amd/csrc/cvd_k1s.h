@@ -54,6 +54,19 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #define CVD_K1S_TRIM 0
 #endif
 constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
+// Word offsets (CVD_K1S_R16, default on): a step's received words enter the cursor and the
+// branch-metric table as byte offsets 16 r, each one v_lshrrev and one v_and of the six-step
+// group's window shifted once -- both take vector or constant operands at ~2.5 cycles per
+// wave64 instruction -- instead of a v_bfe (its shift held in a VGPR) then v_lshlrev /
+// v_lshl_add at ~4.2 each (profiles/r05an); and the two-step records' third word is only
+// extracted when they are compiled in
+#ifndef CVD_K1S_R16
+#define CVD_K1S_R16 1
+#endif
+constexpr bool kR16 = CVD_K1S_R16 != 0;
+// a cursor / step word parameter as the byte offset 16 r, and a raw word r as that parameter
+__device__ __forceinline__ uint32_t word_off16(uint32_t rp) { return kR16 ? rp : 16u * rp; }
+__device__ __forceinline__ uint32_t word_param(uint32_t r) { return kR16 ? 16u * r : r; }
 
 // The lockstep lanes read each 16-B stream chunk once: non-temporal loads (CVD_K1S_NT_STREAM,
 // default on) so that the 131 GB per launch do not evict the row tables' lines from L2 (p = 0.1
@@ -111,7 +124,8 @@ struct BsCursor {
   // entry rn (16 B {log P̂1, successor row, T_ref count c}) of learned row s, dense records
   __device__ void prefetch_row(const ExpArgs& a, int32_t s, uint32_t rn) {
     uint32_t o;
-    asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o) : "v"(rn), "v"((uint32_t)s * 64u));
+    if constexpr (kR16) asm("v_lshl_add_u32 %0, %1, 6, %2" : "=v"(o) : "v"((uint32_t)s), "v"(rn));
+    else asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o) : "v"(rn), "v"((uint32_t)s * 64u));
     const uint4 v = ld_off<uint4>(a.drow, o);
     pc = v.w;
     pnx = (int32_t)v.z;
@@ -122,6 +136,7 @@ struct BsCursor {
   // (every k1s offset is a 32-bit byte offset from the table's base: the host keeps the
   // bit-sliced tables under 4 GiB)
   __device__ void prefetch_t2(const ExpArgs& a, int32_t s, uint32_t rn, uint32_t rnn) {
+    if constexpr (kR16) { rn >>= 4; rnn >>= 4; }
     uint32_t o;
     asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(o) : "v"(rn | (rnn << 2)), "v"((uint32_t)s << 9));
     const uint4 v = ld_off<uint4>(a.t2, o);
@@ -164,7 +179,7 @@ struct BsCursor {
     if (cand) {
       const uint32_t so = slot_off(hs);
       load_image(a.hkey, so + 32u * PH, pkey);
-      const uint4 v = ld_off<uint4>(a.hkey, so + 4u * kBsRecWord + 16u * r);
+      const uint4 v = ld_off<uint4>(a.hkey, so + 4u * kBsRecWord + word_off16(r));
       pc = v.w;
       pnx = (int32_t)v.z;
       plp = __hiloint2double((int)v.y, (int)v.x);
@@ -200,7 +215,7 @@ struct BsCursor {
         for (int pr = 1; pr <= a.max_probe; ++pr) {
           sl = (sl + 1u) & a.hmask;
           const uint32_t so = slot_off(sl);
-          const uint4 v = ld_off<uint4>(a.hkey, so + 4u * kBsRecWord + 16u * r);
+          const uint4 v = ld_off<uint4>(a.hkey, so + 4u * kBsRecWord + word_off16(r));
           if (v.w == 0u) break;
           uint32_t k[8];
           load_image(a.hkey, so + 32u * PH, k);
@@ -286,7 +301,9 @@ struct BsCursor {
 template <int PH, bool kUni>
 __device__ __forceinline__ void bs_step(const ExpArgs& a, BsCursor& cur, const uint32_t (&R)[2][4], uint32_t rr,
                                         uint32_t (&N)[2][4], uint32_t& c) {
-  const uint4* et = bs_etab_lds() + (PH * 4 + rr) * 2;
+  const uint4* et = kR16 ? reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(bs_etab_lds()) + PH * 128 +
+                                                          cvd::bs_shl<1>(rr))
+                        : bs_etab_lds() + (PH * 4 + rr) * 2;
   const uint4 E0 = et[0], E1 = et[1];
   const uint32_t e0[2] = {E0.x, E1.x}, e1[2] = {E0.y, E1.y}, ez[2] = {E0.z, E1.z};
   uint32_t mu;
@@ -342,7 +359,7 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
       plp2 = __hiloint2double((int)v.w, (int)v.z);
       cur.plp = __hiloint2double((int)v.y, (int)v.x);
     } else {
-      cur.prefetch_row(a, cur.slot, x & 3u);
+      cur.prefetch_row(a, cur.slot, word_param(x & 3u));
     }
   };
   uint32_t mode = kWalkDone;
@@ -363,7 +380,7 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   // one ACS step of the wave at phase PH (every lane computes; ACS lanes keep the result)
   auto acs_step = [&](auto phc) {
     constexpr int PH = decltype(phc)::value;
-    const uint32_t rr = word_at() & 3u;
+    const uint32_t rr = word_param(word_at() & 3u);
     uint32_t Nn[2][4], c;
     bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
     if (mode == kWalkAcs) {
@@ -523,7 +540,7 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     int64_t wi = 0;
     uint32_t sh = 0u;
     BsCursor cur;
-    cur.start(a, cw & 3u, (cw >> 2) & 3u);
+    cur.start(a, word_param(cw & 3u), word_param((cw >> 2) & 3u));
     if (CVD_K1S_ABL & 1) cur.h2wave = hmask == 0u;
     auto step = [&](auto phc, uint32_t rr, uint32_t rn, uint32_t rnn) {
       constexpr int PH = decltype(phc)::value;
@@ -539,14 +556,26 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     };
     int64_t t = 0;
     int grp = 0, dec = 0;
+    // word k / 2 of the group's window as the step's parameter (kR16: bits k, k + 1 of win sit
+    // at k + 5, k + 6 of w5 = win << 5, so (w5 >> (k + 1)) & 0x30 = 16 r)
+    auto wk = [&](uint32_t win, uint32_t w5, auto kc) -> uint32_t {
+      constexpr uint32_t k = decltype(kc)::value;
+      if constexpr (kR16) return (w5 >> (k + 1)) & 0x30u;
+      else return bits2(win, k);
+    };
+    auto w3 = [&](uint32_t win, uint32_t w5, auto kc) -> uint32_t {   // the T2 records' third word
+      if constexpr (kK1sT2 || !kR16) return wk(win, w5, kc);
+      else return 0u;
+    };
     for (; t + 6 <= N; t += 6) {
       const uint32_t win = __builtin_amdgcn_alignbit(nw, cw, sh);
-      step(IntC<0>{}, bits2(win, 0), bits2(win, 2), bits2(win, 4));
-      step(IntC<1>{}, bits2(win, 2), bits2(win, 4), bits2(win, 6));
-      step(IntC<2>{}, bits2(win, 4), bits2(win, 6), bits2(win, 8));
-      step(IntC<3>{}, bits2(win, 6), bits2(win, 8), bits2(win, 10));
-      step(IntC<4>{}, bits2(win, 8), bits2(win, 10), bits2(win, 12));
-      step(IntC<5>{}, bits2(win, 10), bits2(win, 12), bits2(win, 14));
+      const uint32_t w5 = kR16 ? win << 5 : 0u;
+      step(IntC<0>{}, wk(win, w5, IntC<0>{}), wk(win, w5, IntC<2>{}), w3(win, w5, IntC<4>{}));
+      step(IntC<1>{}, wk(win, w5, IntC<2>{}), wk(win, w5, IntC<4>{}), w3(win, w5, IntC<6>{}));
+      step(IntC<2>{}, wk(win, w5, IntC<4>{}), wk(win, w5, IntC<6>{}), w3(win, w5, IntC<8>{}));
+      step(IntC<3>{}, wk(win, w5, IntC<6>{}), wk(win, w5, IntC<8>{}), w3(win, w5, IntC<10>{}));
+      step(IntC<4>{}, wk(win, w5, IntC<8>{}), wk(win, w5, IntC<10>{}), w3(win, w5, IntC<12>{}));
+      step(IntC<5>{}, wk(win, w5, IntC<10>{}), wk(win, w5, IntC<12>{}), w3(win, w5, IntC<14>{}));
       sh += 12u;
       if (sh >= 32u) {
         sh -= 32u;
@@ -567,11 +596,12 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     // last 1-5 steps
     if (t < N) {
       const uint32_t win = __builtin_amdgcn_alignbit(nw, cw, sh);
-      step(IntC<0>{}, bits2(win, 0), bits2(win, 2), bits2(win, 4));
-      if (t + 1 < N) step(IntC<1>{}, bits2(win, 2), bits2(win, 4), bits2(win, 6));
-      if (t + 2 < N) step(IntC<2>{}, bits2(win, 4), bits2(win, 6), bits2(win, 8));
-      if (t + 3 < N) step(IntC<3>{}, bits2(win, 6), bits2(win, 8), bits2(win, 10));
-      if (t + 4 < N) step(IntC<4>{}, bits2(win, 8), bits2(win, 10), bits2(win, 12));
+      const uint32_t w5 = kR16 ? win << 5 : 0u;
+      step(IntC<0>{}, wk(win, w5, IntC<0>{}), wk(win, w5, IntC<2>{}), w3(win, w5, IntC<4>{}));
+      if (t + 1 < N) step(IntC<1>{}, wk(win, w5, IntC<2>{}), wk(win, w5, IntC<4>{}), w3(win, w5, IntC<6>{}));
+      if (t + 2 < N) step(IntC<2>{}, wk(win, w5, IntC<4>{}), wk(win, w5, IntC<6>{}), w3(win, w5, IntC<8>{}));
+      if (t + 3 < N) step(IntC<3>{}, wk(win, w5, IntC<6>{}), wk(win, w5, IntC<8>{}), w3(win, w5, IntC<10>{}));
+      if (t + 4 < N) step(IntC<4>{}, wk(win, w5, IntC<8>{}), wk(win, w5, IntC<10>{}), w3(win, w5, IntC<12>{}));
     }
     if (a.sums) {
       const int64_t qe = qwave + lane_id();
