@@ -240,10 +240,20 @@ def main():
     if a.fused:
         a.overlap = 0
     if a.overlap < 0:
-        a.overlap = int(not info["kind"])
+        # the next batch's generator on its own queue, beside the detector: for the dense table
+        # kernel (kind 0), and for persistent detector launches (k1s), whose retiring waves the
+        # generator's blocks follow -- +1.1% at m6 (profiles/r05bd2); the m = 6 butterfly
+        # kernel's block launches lost ~2% to it (profiles/r04y)
+        persistent = any(mm.info().get("persist_seqs", 0) > 0 for mm in models.values())
+        a.overlap = int(not info["kind"] or persistent)
     buf_bytes = det.words_per_seq(N) * 4 * 2 * B
-    if a.overlap and 2 * buf_bytes > (120 << 30):
-        a.overlap = 0                          # two batches would not leave HBM headroom
+    if a.overlap:
+        # two stream buffers must fit the free HBM with 16 GiB to spare (the m6 headline's two
+        # are 2 x 131 GB; CVD_BENCH_OVERLAP_CAP_GB sets the limit instead)
+        cap = os.environ.get("CVD_BENCH_OVERLAP_CAP_GB")
+        free_b = torch.cuda.mem_get_info(det.device)[0] if torch.cuda.is_available() else 0
+        if 2 * buf_bytes > ((int(cap) << 30) if cap else free_b - (16 << 30)):
+            a.overlap = 0
     per_step = npg if sweep_all else 1        # grid points (launch units) per step
 
     def units(s):
@@ -615,6 +625,8 @@ def main():
     }
     if early_out is not None:
         out["early_decision"] = early_out
+    bufs.clear()                               # the stream buffers (up to 2 x 131 GB) before the legs below
+    torch.cuda.empty_cache()
     if a.cpu_baseline and world == 1 and not parity:
         host = host_info(a.cpu_threads)
         out["cpu_baseline"], _ = cpu_baseline(cc, k, n, m, N, a.seed, a.learn_len, a.cpu_seconds, host)
