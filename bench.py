@@ -175,11 +175,103 @@ def launch_ranks(a):
     return subprocess.call(cmd)
 
 
+def _smi(args, timeout=20):
+    """rocm-smi's JSON for `args` (a child process; {} when the tool or the query fails)."""
+    try:
+        out = subprocess.run(["rocm-smi"] + args + ["--json"], capture_output=True, text=True, timeout=timeout)
+        txt = out.stdout
+        return json.loads(txt[txt.index("{"):]) if "{" in txt else {}
+    except (OSError, ValueError, subprocess.SubprocessError):
+        return {}
+
+
+def _visible_cards(d):
+    """the rocm-smi card entries of the GPU(s) this process may use (HIP/ROCR visibility lists
+    index the host's cards in rocm-smi's order; without one, every card)."""
+    cards = sorted((k for k in d if k.startswith("card")), key=lambda k: int(k[4:]) if k[4:].isdigit() else 0)
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES") or \
+        os.environ.get("CUDA_VISIBLE_DEVICES")
+    if vis:
+        try:
+            idx = [int(x) for x in vis.split(",") if x.strip() != ""]
+            sel = [cards[i] for i in idx if 0 <= i < len(cards)]
+            if sel:
+                return sel
+        except ValueError:
+            pass
+    return cards
+
+
+def box_identity():
+    """The box and its GPU before this process touches the GPU (rocm-smi in a child process):
+    product, serial / unique id, power cap, the clock levels, and the idle clocks.  Boxes differ
+    by a few per cent on the same tree; the record makes that attributable."""
+    ident = _smi(["--showproductname", "--showserial", "--showuniqueid", "--showmaxpower", "--showdriverversion"])
+    clk = _smi(["--showclocks", "--showtemp", "--showpower"])
+    cards = _visible_cards(ident) or _visible_cards(clk)
+    keep = ("Card Series", "Card SKU", "Card model", "GFX Version", "Serial Number", "Unique ID",
+            "Max Graphics Package Power (W)", "Driver version")
+    out = {"hostname": socket.gethostname(), "cards": {}}
+    for c in cards:
+        e = {k: v for k, v in ident.get(c, {}).items() if any(s in k for s in keep)}
+        e["idle"] = {k: v for k, v in clk.get(c, {}).items() if "clk" in k.lower() or "Temperature" in k
+                     or "Power" in k}
+        out["cards"][c] = e
+    drv = ident.get("system", {}).get("Driver version")
+    if drv:
+        out["driver"] = drv
+    if not cards:
+        out["note"] = "rocm-smi gave no card records"
+    return out
+
+
+class ClockSampler:
+    """rocm-smi's current clocks, power and temperature of the visible card(s), sampled from a
+    host thread every `period` s while the timed region runs (child processes; no GPU call from
+    this process).  summary() gives each field's median over the samples."""
+
+    def __init__(self, period=4.0):
+        import threading
+        self.period, self.samples, self._stop = period, [], threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.is_set():
+            d = _smi(["--showclocks", "--showpower", "--showtemp"], timeout=15)
+            cards = _visible_cards(d)
+            if cards:
+                self.samples.append({c: d[c] for c in cards})
+            self._stop.wait(self.period)
+
+    def start(self):
+        self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        self._t.join(timeout=30)
+
+    def summary(self):
+        import re
+        vals = {}
+        for s in self.samples:
+            for c, e in s.items():
+                for k, v in e.items():
+                    m = re.search(r"(-?\d+(?:\.\d+)?)\s*(Mhz|MHz|W)?\)?\s*$", str(v))
+                    if m and ("clk" in k.lower() or "Power" in k or "Temperature" in k):
+                        vals.setdefault(c, {}).setdefault(k, []).append(float(m.group(1)))
+        med = {c: {k: sorted(v)[len(v) // 2] for k, v in e.items()} for c, e in vals.items()}
+        return {"samples": len(self.samples), "period_s": self.period, "median_under_load": med}
+
+
 def main():
     a = parse()
     rc = launch_ranks(a)
     if rc is not None:
         sys.exit(rc)
+    # (before any GPU call: rocm-smi in child processes)
+    box = box_identity() if int(os.environ.get("RANK", "0")) == 0 and os.environ.get("CVD_BENCH_SMI", "1") != "0" \
+        else None
     import numpy as np
     import torch
     from __graft_entry__ import load_package
@@ -239,21 +331,30 @@ def main():
         a.fused = int(not parity and bool(info["mc_fused"]))   # where it measured faster (cvd_model_info)
     if a.fused:
         a.overlap = 0
+    overlap_rec = {"requested": a.overlap}
     if a.overlap < 0:
         # the next batch's generator on its own queue, beside the detector: for the dense table
         # kernel (kind 0), and for persistent detector launches (k1s), whose retiring waves the
         # generator's blocks follow -- +1.1% at m6 (profiles/r05bd2); the m = 6 butterfly
-        # kernel's block launches lost ~2% to it (profiles/r04y)
+        # kernel's block launches lost ~2% to it (profiles/r04y).  --sweep all keeps its
+        # multi-model launches unless --overlap 1 is passed
         persistent = any(mm.info().get("persist_seqs", 0) > 0 for mm in models.values())
-        a.overlap = int(not info["kind"] or persistent)
+        a.overlap = int((not info["kind"] or persistent) and not (sweep_all and a.multi and not parity))
+        overlap_rec["auto"] = {"dense_table": not info["kind"], "persistent_detector": persistent,
+                               "sweep_all_multi_kept": bool(sweep_all and a.multi and not parity)}
     buf_bytes = det.words_per_seq(N) * 4 * 2 * B
     if a.overlap:
         # two stream buffers must fit the free HBM with 16 GiB to spare (the m6 headline's two
         # are 2 x 131 GB; CVD_BENCH_OVERLAP_CAP_GB sets the limit instead)
         cap = os.environ.get("CVD_BENCH_OVERLAP_CAP_GB")
         free_b = torch.cuda.mem_get_info(det.device)[0] if torch.cuda.is_available() else 0
-        if 2 * buf_bytes > ((int(cap) << 30) if cap else free_b - (16 << 30)):
+        limit = (int(cap) << 30) if cap else free_b - (16 << 30)
+        overlap_rec.update({"free_bytes": free_b, "two_buffers_bytes": 2 * buf_bytes, "limit_bytes": limit,
+                            "limit_source": "CVD_BENCH_OVERLAP_CAP_GB" if cap else "free HBM - 16 GiB"})
+        if 2 * buf_bytes > limit:
             a.overlap = 0
+            overlap_rec["turned_off"] = "two stream buffers exceed the limit"
+    overlap_rec["on"] = bool(a.overlap)
     per_step = npg if sweep_all else 1        # grid points (launch units) per step
 
     def units(s):
@@ -387,6 +488,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ev = make_events(a.steps)
+    sampler = ClockSampler().start() if box is not None else None
     t0 = time.perf_counter()
     run(a.steps, 0, ev)
     shard = counts.clone() if dist else None   # this rank's own counts (reduce_record checks the reduce)
@@ -397,6 +499,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if sampler is not None:
+        sampler.stop()
+        box["under_load"] = sampler.summary()
+
     def max_over_ranks(x):
         # RCCL reduces device tensors only; gloo host tensors
         t = torch.tensor(x if isinstance(x, list) else [x], device=det.device if a.dist_backend == "nccl" else "cpu",
@@ -542,17 +648,39 @@ def main():
             # per launch from the counter pass, over this run's live launch time
             winst = ipws * (2 * B * len(groups[gdom]) / 64) * N    # the dominant launch
             ach = winst / (det_ms * 1e-3)
-            cpi = pmc.get("valu_cycles_per_inst")
+            # (counted instructions at the 2-cycle wave64 issue rate; round 5's modelled issue-cycle
+            # fraction -- a static instruction mix priced per opcode -- read above 1 at p = 0.02 and
+            # is no longer reported)
             valu = {"insts_per_wave_step": ipws, "achieved": ach, "peak": VALU_PEAK_WINST,
                     "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WINST,
-                    # the same instructions priced at their measured issue cost per opcode and
-                    # operand kind (~2.4-2.8 cycles for bitop3 / logic / add / lshr with vector or
-                    # constant sources, ~4.2-4.6 with a scalar source and for the other opcodes;
-                    # profiles/valu_issue_cycles_r05.json) instead of 2 cycles each
-                    "cycles_per_inst": cpi,
-                    "issue_cycle_weighted_frac": (ach * cpi / (1024 * SHADER_GHZ * 1e9)) if cpi else None,
-                    "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU, instruction mix x "
-                              "profiles/valu_issue_cycles_r05.json) + live HIP-event time of the launch"}
+                    "source": os.path.relpath(a.pmc_traffic, ROOT) + " (SQ_INSTS_VALU) + live HIP-event time "
+                              "of the launch"}
+            # where the detector's wave-cycles go (SQ_WAVE_CYCLES = ACTIVE_INST_ANY + WAIT_ANY +
+            # WAIT_INST_ANY, MI355X_MICROARCH.md), launch-weighted over the sweep
+            cpl = pmc.get("counters_per_launch") or {}
+            wc = cpl.get("SQ_WAVE_CYCLES")
+            if wc:
+                valu["wave_cycles_split"] = {k: cpl.get(c, 0.0) / wc for k, c in (
+                    ("issuing", "SQ_ACTIVE_INST_ANY"), ("waiting_on_memory_or_barrier", "SQ_WAIT_ANY"),
+                    ("issue_stalled", "SQ_WAIT_INST_ANY"))}
+    # What bounds the m = 6 detector (k1s): dependent row-lookup latency, not HBM bandwidth and
+    # not VALU issue.  The ablations it rests on: removing 5% of the step's
+    # modelled VALU issue cycles (CVD_BS_VFAST) gained <= 1% at p >= 0.05 (profiles/r05aq);
+    # four machine-scheduler strategies land within 0.1% (profiles/r05ae), so instruction order
+    # does not matter; skipping only the H2 waves' L2 filter reads (timing only) shortens p = 0.2
+    # by 9% (profiles/r05w); with the H1 waves' candidate lines cold (profiles/r06_lookup_study.py:
+    # 90-94% of H1 wave-steps at p = 0.05 / 0.1 hold a lane that re-enters a row from a directory
+    # line, 9% / 4% of those rows among the 16k hottest) the waves wait on memory 46-50% of their
+    # cycles at 4 waves per SIMD (SQ_WAIT_ANY, roofline.valu.wave_cycles_split).
+    latency_bound = (not parity and not lds_diag and info.get("kind") == 1 and info.get("explicit_kernel") == 5)
+    bound_basis = None
+    if latency_bound:
+        bound_basis = ("dependent row lookups (L2 / Infinity Cache latency) at 4 waves per SIMD: -5% modelled VALU "
+                       "issue -> <= 1% measured at p >= 0.05 (profiles/r05aq); scheduler strategies within 0.1% "
+                       "(profiles/r05ae); H2 filter reads skipped (timing only) -> p = 0.2 -9% (profiles/r05w); waves "
+                       "wait on memory 46-50% of their cycles (SQ_WAIT_ANY, valu.wave_cycles_split)")
+    elif lds_diag:
+        bound_basis = "LDS array busy (roofline.lds, profiles/pmc_lds_<config>.json)"
     c = counts.cpu().numpy()
     per_p = {str(p): {"Pd": float(c[i, 0]) / max(1, steps_at[i] * B * world),
                       "Pc": float(c[i, 0] + c[i, 1]) / max(1, 2 * steps_at[i] * B * world),
@@ -592,7 +720,8 @@ def main():
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "distributed": dist_rec,
-        "roofline": {"bound": "lds" if lds_diag else "valu" if valu else "hbm", "achieved": achieved,
+        "roofline": {"bound": "lds" if lds_diag else ("latency" if latency_bound else "hbm"), "achieved": achieved,
+                     "bound_basis": bound_basis,
                      "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "lds": lds_diag,
@@ -610,7 +739,8 @@ def main():
                      "detector_launches_per_step": len(groups), "detector_ms_per_step": phase_ms,
                      "valu": valu},
         "diagnostic": {"generator_ms_per_step": gen_ms, "detector_ms_per_step": phase_ms,
-                       "overlap": bool(a.overlap), "fused": bool(a.fused), "model_setup_s": t_setup,
+                       "overlap": bool(a.overlap), "overlap_decision": overlap_rec, "fused": bool(a.fused),
+                       "model_setup_s": t_setup,
                        "setup_by_rank": setup_by_rank,
                        "multi_model_launches": use_multi,
                        "seq_steps_per_s_detector": 2 * B * per_step * N / (phase_ms * 1e-3),
@@ -625,6 +755,7 @@ def main():
     }
     if early_out is not None:
         out["early_decision"] = early_out
+    out["box"] = box
     bufs.clear()                               # the stream buffers (up to 2 x 131 GB) before the legs below
     torch.cuda.empty_cache()
     if a.cpu_baseline and world == 1 and not parity:
@@ -777,7 +908,7 @@ def run_c4(a, pkg, world, rank, local, dist):
                    "learn_len": a.learn_len, "early_decision": False,
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "per_N": per_N,
-        "roofline": {"bound": "valu", "achieved": sum(per_N[str(N)]["roofline"]["algorithmic_bytes"] for N in Ns)
+        "roofline": {"bound": "latency", "achieved": sum(per_N[str(N)]["roofline"]["algorithmic_bytes"] for N in Ns)
                      / elapsed / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": sum(per_N[str(N)]["roofline"]["algorithmic_bytes"] for N in Ns) / elapsed / 1e9 / HBM_PEAK_GBS,
                      "traffic": None,

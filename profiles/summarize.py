@@ -89,7 +89,10 @@ def main(src, name):
                "SALU_insts_per_wave_step": c.get("SQ_INSTS_SALU", 0.0) / (waves * N),
                "VMEM_RD_insts_per_wave_step": c.get("SQ_INSTS_VMEM_RD", 0.0) / (waves * N),
                "wait_any_frac_of_wave_cycles": c.get("SQ_WAIT_ANY", 0.0) / max(1.0, c.get("SQ_WAVE_CYCLES", 1.0)),
-               "active_valu_frac_of_wave_cycles": c.get("SQ_ACTIVE_INST_VALU", 0.0) / max(1.0, c.get("SQ_WAVE_CYCLES", 1.0)),
+               # SQ_ACTIVE_INST_VALU reads SQ_INSTS_VALU to the last digit on gfx950 (profiles/r05bg_m6
+               # pmc2 / pmc3): an instruction count, not cycles -- not reported as a fraction
+               "issuing_frac_of_wave_cycles": c.get("SQ_ACTIVE_INST_ANY", 0.0) / max(1.0, c.get("SQ_WAVE_CYCLES", 1.0)),
+               "issue_stalled_frac_of_wave_cycles": c.get("SQ_WAIT_INST_ANY", 0.0) / max(1.0, c.get("SQ_WAVE_CYCLES", 1.0)),
                "kernel_cycles": kc}
         if ms is not None:
             out["detector_ms_live"] = ms
@@ -134,7 +137,8 @@ def main(src, name):
         "GRBM_GUI_ACTIVE": per.get("GRBM_GUI_ACTIVE"),
         "kernel_cycles": kernel_cycles,
         "wait_inst_any_frac_of_wave_cycles": per.get("SQ_WAIT_INST_ANY", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
-        "active_valu_frac_of_wave_cycles": per.get("SQ_ACTIVE_INST_VALU", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
+        "issuing_frac_of_wave_cycles": per.get("SQ_ACTIVE_INST_ANY", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
+        "wait_any_frac_of_wave_cycles": per.get("SQ_WAIT_ANY", 0.0) / max(1.0, per.get("SQ_WAVE_CYCLES", 1.0)),
         "counters_per_launch": per,
         "generator": {
             "kernel": "gen_fast_kernel (encoder + BSC noise, two launches per step: H1, H2)",
@@ -154,35 +158,9 @@ def main(src, name):
         "batch": B,
         "N": N,
     }
-    # cycle-weighted VALU issue fraction: the step loop's opcode mix (static ISA of
-    # the kernel this tree builds, profiles/isa_breakdown.py) priced with the measured
-    # issue cost per class (profiles/valu_issue_cycles.json), times the dynamic
-    # instruction count, over the launch's SIMD-cycles
-    if out["detector"] == "markov" and "k1b" in out["kernel"]:
-        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-        import isa_breakdown
-        import valu_model
-        import tempfile
-        bs = "bit-sliced" in out["kernel"]    # k1s: six steps per loop trip (isa_breakdown)
-        with tempfile.TemporaryDirectory() as d:
-            lines = isa_breakdown.build_isa(out["config"], ["-DCVD_K1B_BITSLICE=1"] if bs else [],
-                                            os.path.join(d, "k.s"))
-        mix = {}
-        for _name, ins in isa_breakdown.blocks(isa_breakdown.main_loop(lines, 1 if bs else 0)):
-            for x in ins:
-                if x.startswith("v_"):
-                    mix[x.strip()] = mix.get(x.strip(), 0) + (1 / 6 if bs else 0.25)
-        # round 5: priced per instruction line, operands included (valu_model.line_cycles_r05)
-        avg, by_class = valu_model.weighted_line_cycles(mix)
-        out["valu_cycles_per_inst"] = avg
-        out["valu_cycles_source"] = ("static instruction mix of the step loop (profiles/isa_breakdown.py) x measured "
-                                     "issue cost per opcode and operand kind (profiles/valu_issue_cycles_r05.json, "
-                                     "profiles/r05an)")
-        out["valu_mix_by_class_per_step"] = by_class
-        out["valu_issue_cycle_frac"] = per.get("SQ_INSTS_VALU", 0.0) * avg / (1024 * max(1.0, kernel_cycles))
-        for e in out["per_p"].values():
-            c = e["counters_per_launch"]
-            e["valu_issue_cycle_frac"] = c.get("SQ_INSTS_VALU", 0.0) * avg / (1024 * max(1.0, e["kernel_cycles"]))
+    # (round 5 priced the step loop's static instruction mix per opcode into a "VALU issue
+    # cycle fraction"; it read 1.015 at p = 0.02, i.e. the model overcounts, and is dropped: the
+    # counted SQ_INSTS_VALU at the 2-cycle rate and the wave-cycle split above are what is measured)
     fn = f"pmc_{out['detector']}_{out['config']}.json"
     json.dump(out, open(os.path.join(ROOT, "profiles", fn), "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k not in ("counters_per_launch", "per_p")}, indent=1))
