@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CVD_LIB_PATH: another build of the same ABI (A/B builds, profiles/build_ab.sh)
 LIB_PATH = os.environ.get("CVD_LIB_PATH") or os.path.join(_HERE, "lib", "libcvd.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 PATH_AUTO, PATH_TABLE, PATH_EXPLICIT, PATH_EXPLICIT_GENERIC, PATH_EXPLICIT_ORBIT, PATH_EXPLICIT_BUTTERFLY = 0, 1, 2, 3, 4, 5
 DETECT_EARLY_DECISION = 0x100   # OR'ed into path: counts only, stop once every decision is certain
@@ -111,6 +111,7 @@ EXPORTS = {
                                        ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     "cvd_model_device_error": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
+    "cvd_chunk_last": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int64)]),
     "cvd_mc_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_code),
                                     ctypes.c_double, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
@@ -156,3 +157,12 @@ def check(rc):
         msg = lib().cvd_last_error().decode(errors="replace")
         raise CvdError(f"libcvd error {rc}: {msg}")
     return rc
+
+
+def chunk_last():
+    """The chunked launches of this process's last detect call (cvd_chunk_last): groups (0:
+    the call ran unchunked), chunks per sequence C, steps per chunk L, and the sequences left
+    to the sequential rerun."""
+    out = (ctypes.c_int64 * 4)()
+    check(lib().cvd_chunk_last(out))
+    return {"groups": int(out[0]), "C": int(out[1]), "L": int(out[2]), "reruns": int(out[3])}

@@ -177,7 +177,14 @@ struct ExpArgs {
   int32_t* err;             // error flags (nullable): bit 0 = k1b_walk left its loop by the guard
   const uint32_t* pf;       // k1s LDS pre-filter (CVD_K1S_PF): 2^kBsPfLog2Bits bits, copied into dynamic LDS
   uint32_t* wq;             // k1s persistent launch: work-queue counter (zeroed before the launch), else null
+  // chunked detection (k1s, counts via ck_combine_kernel): unit u runs time chunk
+  // u % ck_n of the 64 sequences of wave u / ck_n -- steps [j ck_len, (j + 1) ck_len), started
+  // ck_warm steps early from D = 0 -- and writes its record to ck_out instead of sums / counts
+  int32_t ck_n;             // chunks per sequence (0: off)
+  int32_t ck_len, ck_warm;  // steps per chunk and warm-up steps (multiples of 192)
+  uint32_t* ck_out;         // [ck_n][nseq][kCkRecWords]: D at the chunk start and end (phase 0), lp, lr
 };
+constexpr int kCkRecWords = 20;   // chunk record: D_start planes [0, 8), D_end planes [8, 16), lp, lr (f64)
 
 // Received words of one sequence, one word of lookahead (the next step's r is
 // known before the current step ends, so its P̂1 row entry can be prefetched).

@@ -3,6 +3,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <array>
 #include <string>
 #include <vector>
 
@@ -101,7 +102,6 @@ struct cvd_model {
   uint32_t* d_bkey = nullptr;
   uint32_t* d_bdkey = nullptr;
   uint32_t* d_bpf = nullptr;
-  uint32_t* d_wq = nullptr;       // k1s persistent launches: kWqRing work-queue counters
   uint32_t* d_bmp = nullptr;
   uint32_t* d_bmk1 = nullptr;
   uint32_t* d_bfly = nullptr;
@@ -171,6 +171,9 @@ int64_t multi_variant(const cvd_model& M);
 // sequences above which a launch of the model is persistent (cvd_model_info.persist_seqs; 0:
 // never), and the block count of such a launch over nseq sequences (0: a block launch)
 int64_t persist_seqs(const cvd_model& M);
+// the last detect call's chunked launches (cvd_kernels.hip): {chunked groups,
+// chunks per sequence C, steps per chunk L, sequences rerun sequentially}; cvd_chunk_last
+extern std::array<int64_t, 4> ck_last;
 int64_t persist_grid(const cvd_model& M, int64_t nseq);
 
 // P̂1 learning chain on the GPU (cvd_learn.hip): identical outputs to the host chain.

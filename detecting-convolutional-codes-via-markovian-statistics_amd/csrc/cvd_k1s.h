@@ -54,6 +54,11 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #define CVD_K1S_TRIM 0
 #endif
 constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
+// chunked launches (-DCVD_K1S_CK=0 compiles them out, for A/Bs of the unchunked
+// loop's code: the host then must not chunk, CVD_CHUNK=0)
+#ifndef CVD_K1S_CK
+#define CVD_K1S_CK 1
+#endif
 // Word offsets (CVD_K1S_R16, default on): a step's received words enter the cursor and the
 // branch-metric table as byte offsets 16 r, each one v_lshrrev and one v_and of the six-step
 // group's window shifted once -- both take vector or constant operands at ~2.5 cycles per
@@ -497,8 +502,21 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
 }
 
 // one wave's 64 sequences [64 gw, 64 gw + 64) through the lockstep loop, or walk mode
-template <uint64_t XM>
-__device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const double* s_lt) {
+// chunked detection (a.ck_n > 0): a lane's 8 plane words into its chunk record
+// (dword `off`: 0 = D at the chunk start, 8 = D at its end; both in layout phase 0)
+__device__ __forceinline__ void ck_store(const ExpArgs& a, int64_t qwave, int32_t j, uint32_t off,
+                                         const uint32_t (&R)[2][4]) {
+  uint32_t l = lane_id();
+  asm volatile("" : "+v"(l));   // (keeps the address arithmetic in the rarely taken branch)
+  uint4* p = reinterpret_cast<uint4*>(a.ck_out + ((size_t)j * (size_t)a.nseq + (size_t)qwave + l) * kCkRecWords + off);
+  p[0] = make_uint4(R[0][0], R[0][1], R[0][2], R[0][3]);
+  p[1] = make_uint4(R[1][0], R[1][1], R[1][2], R[1][3]);
+}
+
+// (kCk: a chunked launch's unit; a separate instantiation, so that the unchunked loop keeps its
+// registers and scalar state exactly)
+template <uint64_t XM, bool kCk = false>
+__device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const double* s_lt, int32_t ck_j = 0) {
   constexpr bool kUni = xm_uni<6, XM>();
   if (a.walk) {
     // H1 and H2 waves alternate on every SIMD (k1b_body)
@@ -520,6 +538,16 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     asm volatile("" : "+v"(lpu));
     const int64_t N = a.N, nwords = (N + 15) / 16;
     const size_t cstride = (size_t)a.nseq * 4;
+    // the steps this unit runs: all of them, or (chunked) its chunk [t_sum, t_end) after
+    // t_sum - t_begin warm-up steps from D = 0 whose sums it drops (every bound but N a multiple
+    // of 192: whole 16-B stream chunks and six-step groups, the planes in layout phase 0)
+    constexpr bool ck = kCk;
+    int64_t t_begin = 0, t_sum = 0, t_end = N;
+    if (ck) {
+      t_sum = (int64_t)ck_j * a.ck_len;
+      t_end = min(N, t_sum + (int64_t)a.ck_len);
+      t_begin = max((int64_t)0, t_sum - (int64_t)a.ck_warm);
+    }
     uint32_t c4[4];
     auto load_chunk = [&](int64_t ci) {
       const uint32_t* rb = a.r + (size_t)ci * cstride + (size_t)qwave * 4;
@@ -535,9 +563,9 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     // the received words as a 64-bit window (words wi, wi + 1) and the bit offset of the
     // next step in it (< 32 at the top of a six-step group): one funnel shift per group,
     // one bit-field extract per step
-    load_chunk(0);
-    uint32_t cw = pick(0), nw = pick(1);
-    int64_t wi = 0;
+    int64_t wi = t_begin / 16;
+    load_chunk(wi >> 2);
+    uint32_t cw = pick(wi), nw = pick(wi + 1);
     uint32_t sh = 0u;
     BsCursor cur;
     cur.start(a, word_param(cw & 3u), word_param((cw >> 2) & 3u));
@@ -554,7 +582,7 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
         for (int i = 0; i < 4; ++i) R[r][i] = Nn[r][i];
       cur.next(a, rn, rnn);
     };
-    int64_t t = 0;
+    int64_t t = t_begin;
     int grp = 0, dec = 0;
     // word k / 2 of the group's window as the step's parameter (kR16: bits k, k + 1 of win sit
     // at k + 5, k + 6 of w5 = win << 5, so (w5 >> (k + 1)) & 0x30 = 16 r)
@@ -567,7 +595,12 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
       if constexpr (kK1sT2 || !kR16) return wk(win, w5, kc);
       else return 0u;
     };
-    for (; t + 6 <= N; t += 6) {
+    for (; t + 6 <= t_end; t += 6) {
+      if (ck && t == t_sum) {   // (wave-uniform) the chunk's first summed step: D_t is its start
+        ck_store(a, qwave, ck_j, 0u, R);
+        lp = 0.0;
+        lr = 0.0;
+      }
       const uint32_t win = __builtin_amdgcn_alignbit(nw, cw, sh);
       const uint32_t w5 = kR16 ? win << 5 : 0u;
       step(IntC<0>{}, wk(win, w5, IntC<0>{}), wk(win, w5, IntC<2>{}), w3(win, w5, IntC<4>{}));
@@ -594,14 +627,29 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
       }
     }
     // last 1-5 steps
-    if (t < N) {
+    if (t < t_end) {
+      if (ck && t == t_sum) {   // (a last chunk of fewer than six steps)
+        ck_store(a, qwave, ck_j, 0u, R);
+        lp = 0.0;
+        lr = 0.0;
+      }
       const uint32_t win = __builtin_amdgcn_alignbit(nw, cw, sh);
       const uint32_t w5 = kR16 ? win << 5 : 0u;
       step(IntC<0>{}, wk(win, w5, IntC<0>{}), wk(win, w5, IntC<2>{}), w3(win, w5, IntC<4>{}));
-      if (t + 1 < N) step(IntC<1>{}, wk(win, w5, IntC<2>{}), wk(win, w5, IntC<4>{}), w3(win, w5, IntC<6>{}));
-      if (t + 2 < N) step(IntC<2>{}, wk(win, w5, IntC<4>{}), wk(win, w5, IntC<6>{}), w3(win, w5, IntC<8>{}));
-      if (t + 3 < N) step(IntC<3>{}, wk(win, w5, IntC<6>{}), wk(win, w5, IntC<8>{}), w3(win, w5, IntC<10>{}));
-      if (t + 4 < N) step(IntC<4>{}, wk(win, w5, IntC<8>{}), wk(win, w5, IntC<10>{}), w3(win, w5, IntC<12>{}));
+      if (t + 1 < t_end) step(IntC<1>{}, wk(win, w5, IntC<2>{}), wk(win, w5, IntC<4>{}), w3(win, w5, IntC<6>{}));
+      if (t + 2 < t_end) step(IntC<2>{}, wk(win, w5, IntC<4>{}), wk(win, w5, IntC<6>{}), w3(win, w5, IntC<8>{}));
+      if (t + 3 < t_end) step(IntC<3>{}, wk(win, w5, IntC<6>{}), wk(win, w5, IntC<8>{}), w3(win, w5, IntC<10>{}));
+      if (t + 4 < t_end) step(IntC<4>{}, wk(win, w5, IntC<8>{}), wk(win, w5, IntC<10>{}), w3(win, w5, IntC<12>{}));
+    }
+    if (ck) {   // the chunk's record: D at its end (phase 0 unless it is the last) and its sums
+      ck_store(a, qwave, ck_j, 8u, R);
+      uint32_t l = lane_id();
+      asm volatile("" : "+v"(l));
+      double* ps = reinterpret_cast<double*>(
+          a.ck_out + ((size_t)ck_j * (size_t)a.nseq + (size_t)qwave + l) * kCkRecWords + 16u);
+      ps[0] = lp;
+      ps[1] = lr;
+      return;   // (the decisions: ck_combine_kernel)
     }
     if (a.sums) {
       const int64_t qe = qwave + lane_id();
@@ -610,6 +658,7 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     }
     early_final(dec, lp, lr);
   }
+  if constexpr (kCk) return;
   count_decisions_masked(vmask, hmask, lp, lr, a.counts);
 }
 
@@ -642,6 +691,9 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
   // [0, 2 ceil(units / 2)), whose last unit may hold no sequence
   uint32_t nunits = (uint32_t)((a.nseq + 63) / 64);   // < 2^32 (host: grid and queue limits)
   if (a.walk) nunits = (nunits + 1u) & ~1u;
+  // chunked: ck_n units (time chunks) per wave of sequences (no walk mode)
+  const uint32_t ckn = a.ck_n > 0 ? (uint32_t)a.ck_n : 1u;
+  nunits *= ckn;
   auto take = [&]() -> uint32_t {
     uint32_t u = 0u;
     if (lane_id() == 0) u = atomicAdd(a.wq, 1u);
@@ -649,7 +701,8 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
   };
   uint32_t u = a.wq ? take() : blk * (uint32_t)(kK1bBlock / 64) + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
   while (u < nunits) {
-    k1s_wave<XM>(a, (int64_t)u, s_lt);
+    if (CVD_K1S_CK && a.ck_n > 0) k1s_wave<XM, true>(a, (int64_t)(u / ckn), s_lt, (int32_t)(u % ckn));
+    else k1s_wave<XM>(a, (int64_t)u, s_lt);
     if (!a.wq) break;
     u = take();
   }

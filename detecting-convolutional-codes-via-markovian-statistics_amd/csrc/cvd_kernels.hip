@@ -1446,6 +1446,74 @@ __global__ __launch_bounds__(kBlock, kK1bWavesPerSimd) void detect_k1b_kernel(Ex
   k1b_body<m, false, 0, kTrace>(a, blockIdx.x);
 }
 
+// ──────────── chunked detection: the decisions ────────────
+//
+// The k1s kernel's chunked launch leaves one record per (time chunk j, sequence q): D at the
+// chunk's start and end and the chunk's own fp64 sums.  Per sequence this kernel
+//  * checks the chunks join: chunk j's warm-started D at its start equals chunk j-1's D at its
+//    end (chunk 0 starts from the true D_0 = 0, so every chunk of a joined sequence ran the
+//    reference recursion exactly: the step is a function of D and the word);
+//  * adds the chunk sums in chunk order and decides lp > lr (Pd_plotter.py:215, :222) only
+//    where the decision is certain for the reference's sequential sum as well: all increments
+//    are <= 0 (logs of probabilities), so the sequential sum of N terms and this one are both
+//    within gamma-type bounds of the exact sum, |S_seq - S_chunk| <= (N + L + C) u (1 + o(1))
+//    |S_chunk| with u = 2^-53; with kappa = 4 (N + L + C + 16) u a gap |lp - lr| > 2 kappa
+//    (|lp| + |lr|) decides it;
+//  * counts the decided sequences (one 64-bit atomic per wave and hypothesis) and lists the
+//    others (chunks that did not join, or a gap too small) for the exact sequential rerun.
+__global__ __launch_bounds__(kBlock) void ck_combine_kernel(const uint32_t* ck, int64_t nseq, int64_t n_h1,
+                                                            int32_t C, double kappa, int32_t redo_all,
+                                                            int64_t* counts, int32_t* redo_n, int32_t* redo) {
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = q < nseq, h1 = q < n_h1;
+  bool gt = false, lt = false;
+  if (valid) {
+    bool joined = true;
+    double lp = 0.0, lr = 0.0;
+    for (int32_t j = 0; j < C; ++j) {
+      const uint4* rec = reinterpret_cast<const uint4*>(ck + ((size_t)j * (size_t)nseq + (size_t)q) * kCkRecWords);
+      if (j > 0) {
+        const uint4* prv =
+            reinterpret_cast<const uint4*>(ck + ((size_t)(j - 1) * (size_t)nseq + (size_t)q) * kCkRecWords);
+        const uint4 s0 = rec[0], s1 = rec[1], e0 = prv[2], e1 = prv[3];
+        joined = joined && s0.x == e0.x && s0.y == e0.y && s0.z == e0.z && s0.w == e0.w && s1.x == e1.x &&
+                 s1.y == e1.y && s1.z == e1.z && s1.w == e1.w;
+      }
+      const uint4 v = rec[4];
+      lp += __hiloint2double((int)v.y, (int)v.x);   // chunk order = t order of the chunks
+      lr += __hiloint2double((int)v.w, (int)v.z);
+    }
+    const double d = lp - lr, e = 2.0 * kappa * (fabs(lp) + fabs(lr));
+    if (joined && !redo_all) {
+      gt = d > e;
+      lt = d < -e;
+    }
+    if (!gt && !lt) {
+      const int k = h1 ? 0 : 1;
+      const int32_t i = atomicAdd(redo_n + k, 1);
+      redo[(size_t)k * (size_t)nseq + (size_t)i] = (int32_t)q;
+    }
+  }
+  const uint64_t b1 = __ballot(valid && h1 && gt), b2 = __ballot(valid && !h1 && lt);   // Pd_plotter.py:215, :222
+  if (lane_id() == 0) {
+    if (b1) atomicAdd(reinterpret_cast<unsigned long long*>(counts), (unsigned long long)__popcll(b1));
+    if (b2) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 1), (unsigned long long)__popcll(b2));
+  }
+}
+
+// the listed sequences' streams into a compact buffer (H1 list first, then H2), for the rerun:
+// 16-B chunk c of sequence q at r4[c pitch + q] (cvd.h stream layout)
+__global__ __launch_bounds__(kBlock) void ck_gather_kernel(const uint4* r4, int64_t pitch, int64_t w4,
+                                                           const int32_t* redo, int64_t nseq, int32_t n1, int32_t n2,
+                                                           uint4* out) {
+  const int64_t nr = (int64_t)n1 + n2;
+  const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (idx >= w4 * nr) return;
+  const int64_t c = idx / nr, i = idx - c * nr;
+  const int64_t q = i < n1 ? redo[i] : redo[nseq + (i - n1)];
+  out[c * nr + i] = r4[c * pitch + q];
+}
+
 using ExpKernel = void (*)(ExpArgs);
 ExpKernel pick_k1b(int m, bool trace) {
   switch (m) {
@@ -1810,12 +1878,10 @@ bool cvd::walk_preferred(const cvd_model& M, bool early) {
   return !early && M.kind == 1 && M.learn_len_eff > 0 && ratio * M.n_rows < M.learn_len_eff;
 }
 
-constexpr uint32_t kWqRing = 64;   // work-queue counters per model (persistent k1s launches)
-
 // the persistent launch's blocks (CVD_K1S_PERSIST=0: never; CVD_K1S_PERSIST_BLOCKS=b: at most b,
 // tests), and the sequences above which a launch is persistent
 static int64_t persist_cap(const cvd_model& M) {
-  if (!M.rtc_fn || !M.rtc_bs || !M.d_wq || M.rtc_persist_grid <= 0 || env_i("CVD_K1S_PERSIST", 1) == 0) return 0;
+  if (!M.rtc_fn || !M.rtc_bs || M.rtc_persist_grid <= 0 || env_i("CVD_K1S_PERSIST", 1) == 0) return 0;
   int64_t g = M.rtc_persist_grid;
   if (const int pb = env_i("CVD_K1S_PERSIST_BLOCKS", 0); pb > 0) g = std::min<int64_t>(g, pb);
   return g;
@@ -1861,6 +1927,7 @@ static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int6
   a.err = M.d_err;
   a.pf = bs && M.rtc_pf ? M.d_bpf : nullptr;
   a.wq = nullptr;   // (launch_detect_explicit sets it for a persistent launch)
+  a.ck_n = 0; a.ck_len = 0; a.ck_warm = 0; a.ck_out = nullptr;   // (ck_submit sets them for a chunked launch)
   a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
@@ -1897,13 +1964,15 @@ int cvd::launch_detect_explicit(const cvd_model& M, const uint32_t* d_r, int64_t
     // their sequences from a work queue (k1s_body); its counter, one of a ring per model, is
     // zeroed on the launch's stream
     if (const int64_t pgrid = persist_grid(M, nseq); pgrid > 0) {
-      static std::atomic<uint32_t> seq{0};
-      a.wq = M.d_wq + (seq.fetch_add(1u) % kWqRing);
+      // (the counter is the launch's own: allocated, zeroed and freed on its stream, so
+      // launches of one model on several streams never share one -- ADVICE r05)
+      HIP_CHECK(hipMallocAsync((void**)&a.wq, sizeof(uint32_t), (hipStream_t)stream));
       HIP_CHECK(hipMemsetAsync(a.wq, 0, sizeof(uint32_t), (hipStream_t)stream));
       rgrid = (unsigned)pgrid;
     }
     HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M.rtc_fn, rgrid, 1, 1, blk, 1, 1, lds,
                                     (hipStream_t)stream, args, nullptr));
+    if (a.wq) HIP_CHECK(hipFreeAsync(a.wq, (hipStream_t)stream));
     return CVD_OK;
   }
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
@@ -1939,6 +2008,172 @@ static int launch_multi(const cvd_model* const* models, int32_t i0, int32_t i1, 
   HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M0.rtc_fn_multi, blocks, 1, 1, blk, 1, 1, lds, (hipStream_t)stream,
                                   args, nullptr));
   return CVD_OK;
+}
+
+// ──────────── chunked detection: launches ────────────
+//
+// A launch over fewer sequences than fill the device twice (the reference's own call shape,
+// run_experiment with num_iter = 10,000: 20,000 sequences per p against 262,144 resident lanes)
+// takes as long as one N-step chain.  Chunked, every sequence's N steps are cut into C time
+// chunks of L steps, each started W steps early from D = 0 on a lane of its own (the recursion
+// forgets its start: profiles/r06_coalesce_study.py, no restart of 512 per p un-coalesced after
+// 768 steps at any p in [0.01, 0.5]), so the launch holds C times the lanes.  The counts are the
+// sequential path's exactly: ck_combine_kernel keeps a sequence only if its chunks join and its
+// decision is certain under the error bound of both summation orders; every other sequence is
+// rerun on the sequential kernel.  Counts only (sums and early decision take the sequential path).
+std::array<int64_t, 4> cvd::ck_last = {0, 0, 0, 0};
+struct CkPlan {
+  int32_t C = 0, L = 0, W = 0;
+};
+static int64_t round_up192(int64_t x) { return (x + 191) / 192 * 192; }
+// CVD_CHUNK: -1 (default) where it pays, 0 never, 1 wherever the kernel allows it (tests);
+// CVD_CHUNK_WARM (1152), CVD_CHUNK_UNITS (4 x the resident waves): warm-up steps and target units
+static bool ck_plan(const cvd_model& M, int64_t N, int64_t nseq_total, CkPlan* P) {
+  const int mode = env_i("CVD_CHUNK", -1);
+  if (mode == 0 || !M.rtc_fn || !M.rtc_bs || N <= 0 || N >= ((int64_t)1 << 30) || nseq_total <= 0) return false;
+  const int64_t W = round_up192(std::max(0, env_i("CVD_CHUNK_WARM", 1152)));
+  const int64_t slots = std::max<int64_t>(1, M.rtc_persist_grid) * (M.rtc_block / 64);   // resident waves
+  const int64_t waves = (nseq_total + 63) / 64;
+  if (mode < 0 && waves >= 2 * slots) return false;   // the launch fills the device as it is
+  const int64_t target = env_i("CVD_CHUNK_UNITS", 0) > 0 ? env_i("CVD_CHUNK_UNITS", 0) : 4 * slots;
+  int64_t C = std::max<int64_t>(1, (target + waves - 1) / waves);
+  int64_t L = round_up192((N + C - 1) / C);
+  // the warm-up at most a third of a chunk where it pays (forced: any chunk of >= 192 steps)
+  L = std::max<int64_t>(L, mode < 0 ? std::max<int64_t>(192, 3 * W) : 192);
+  C = (N + L - 1) / L;
+  if (C < 2 || C * waves > (int64_t)UINT32_MAX / 2) return false;
+  P->C = (int32_t)C; P->L = (int32_t)L; P->W = (int32_t)W;
+  return true;
+}
+
+// A chunked group: its models' launches are queued (ck_submit), the decisions and reruns
+// follow once for every group of a call (ck_finish: one stream synchronisation).
+struct CkGroup {
+  std::vector<const cvd_model*> m;
+  std::vector<const uint32_t*> r;
+  std::vector<int64_t> nseq, nh1;
+  std::vector<int64_t*> counts;
+  std::vector<uint32_t*> rec;
+  std::vector<int32_t*> redo;   // per model: [2][nseq] lists
+  int32_t* redo_n = nullptr;    // [models][2]
+  void* ws = nullptr;
+  CkPlan P;
+  int64_t N = 0;
+};
+
+static int ck_submit(CkGroup& g, hipStream_t st) {
+  const int32_t nm = (int32_t)g.m.size();
+  size_t bytes = 0;
+  std::vector<size_t> orec(nm), oredo(nm);
+  for (int32_t i = 0; i < nm; ++i) {
+    orec[i] = bytes;
+    bytes += ((size_t)g.P.C * (size_t)g.nseq[i] * kCkRecWords * 4 + 255) / 256 * 256;
+    oredo[i] = bytes;
+    bytes += ((size_t)2 * (size_t)g.nseq[i] * 4 + 255) / 256 * 256;
+  }
+  const size_t on = bytes;
+  bytes += (size_t)nm * 2 * 4;
+  HIP_CHECK(hipMallocAsync(&g.ws, bytes, st));
+  char* w = static_cast<char*>(g.ws);
+  g.redo_n = reinterpret_cast<int32_t*>(w + on);
+  HIP_CHECK(hipMemsetAsync(g.redo_n, 0, (size_t)nm * 2 * 4, st));
+  g.rec.resize(nm);
+  g.redo.resize(nm);
+  for (int32_t i = 0; i < nm; ++i) {
+    g.rec[i] = reinterpret_cast<uint32_t*>(w + orec[i]);
+    g.redo[i] = reinterpret_cast<int32_t*>(w + oredo[i]);
+  }
+  auto args_of = [&](int32_t i) {
+    const cvd_model& M = *g.m[i];
+    ExpArgs a = exp_args(M, CVD_KERNEL_BUTTERFLY_RTC, g.r[i], g.N, g.nseq[i], g.nh1[i], nullptr, g.counts[i], nullptr,
+                         M.d_bfly, false);
+    a.walk = 0;
+    a.early = 0;
+    a.ck_n = g.P.C; a.ck_len = g.P.L; a.ck_warm = g.P.W; a.ck_out = g.rec[i];
+    return a;
+  };
+  const cvd_model& M0 = *g.m[0];
+  const unsigned blk = (unsigned)M0.rtc_block;
+  const unsigned lds = rtc_dyn_lds(M0);
+  const int64_t wpb = blk / 64;   // units (waves) per block
+  if (nm == 1) {
+    ExpArgs a = args_of(0);
+    const int64_t units = (int64_t)g.P.C * ((g.nseq[0] + 63) / 64);
+    int64_t grid = (units + wpb - 1) / wpb;
+    // more blocks than stay resident: the persistent launch (k1s_body's work queue)
+    if (const int64_t cap = persist_cap(M0); cap > 0 && grid > cap) {
+      HIP_CHECK(hipMallocAsync((void**)&a.wq, sizeof(uint32_t), st));
+      HIP_CHECK(hipMemsetAsync(a.wq, 0, sizeof(uint32_t), st));
+      grid = cap;
+    }
+    void* args[] = {&a};
+    HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M0.rtc_fn, (unsigned)grid, 1, 1, blk, 1, 1, lds, st, args, nullptr));
+    if (a.wq) HIP_CHECK(hipFreeAsync(a.wq, st));
+  } else {
+    MultiArgs ma;
+    ma.nm = 0;
+    int64_t blocks = 0;
+    for (int32_t i = 0; i < nm; ++i) {
+      blocks += ((int64_t)g.P.C * ((g.nseq[i] + 63) / 64) + wpb - 1) / wpb;
+      if (blocks > (int64_t)UINT32_MAX) { set_error("chunked launch: grid too large"); return CVD_E_INVALID; }
+      ma.a[ma.nm] = args_of(i);
+      ma.blk_end[ma.nm] = (uint32_t)blocks;
+      ++ma.nm;
+    }
+    for (int j = ma.nm; j < kMultiMax; ++j) ma.blk_end[j] = (uint32_t)blocks;
+    void* args[] = {&ma};
+    HIP_CHECK(hipModuleLaunchKernel((hipFunction_t)M0.rtc_fn_multi, (unsigned)blocks, 1, 1, blk, 1, 1, lds, st, args,
+                                    nullptr));
+  }
+  const double kappa = 4.0 * (double)(g.N + g.P.L + g.P.C + 16) * 0x1p-53;
+  const int32_t redo_all = env_i("CVD_CHUNK_REDO_ALL", 0);   // (tests: the rerun path for every sequence)
+  for (int32_t i = 0; i < nm; ++i) {
+    const unsigned grid = (unsigned)((g.nseq[i] + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(ck_combine_kernel, dim3(grid), dim3(kBlock), 0, st, g.rec[i], g.nseq[i], g.nh1[i], g.P.C, kappa,
+                       redo_all, g.counts[i], g.redo_n + 2 * i, g.redo[i]);
+    HIP_CHECK(hipGetLastError());
+  }
+  return CVD_OK;
+}
+
+// the decisions' loose ends: the sequences ck_combine_kernel could not keep, rerun sequentially
+static int ck_finish(std::vector<CkGroup>& gs, hipStream_t st) {
+  if (gs.empty()) return CVD_OK;
+  std::vector<std::vector<int32_t>> rn(gs.size());
+  for (size_t x = 0; x < gs.size(); ++x) {
+    rn[x].resize(2 * gs[x].m.size());
+    HIP_CHECK(hipMemcpyAsync(rn[x].data(), gs[x].redo_n, rn[x].size() * 4, hipMemcpyDeviceToHost, st));
+  }
+  HIP_CHECK(hipStreamSynchronize(st));
+  int rc = CVD_OK;
+  for (size_t x = 0; x < gs.size() && rc == CVD_OK; ++x) {
+    CkGroup& g = gs[x];
+    for (size_t i = 0; i < g.m.size() && rc == CVD_OK; ++i) {
+      const int32_t n1 = rn[x][2 * i], n2 = rn[x][2 * i + 1];
+      if (n1 + n2 == 0) continue;
+      const int64_t w4 = ((g.N + 15) / 16 + 3) / 4, nr = (int64_t)n1 + n2;
+      void* buf = nullptr;
+      HIP_CHECK(hipMallocAsync(&buf, (size_t)(w4 * nr) * 16, st));
+      const unsigned grid = (unsigned)((w4 * nr + kBlock - 1) / kBlock);
+      hipLaunchKernelGGL(ck_gather_kernel, dim3(grid), dim3(kBlock), 0, st, reinterpret_cast<const uint4*>(g.r[i]),
+                         g.nseq[i], w4, g.redo[i], g.nseq[i], n1, n2, static_cast<uint4*>(buf));
+      HIP_CHECK(hipGetLastError());
+      rc = launch_detect_explicit(*g.m[i], static_cast<const uint32_t*>(buf), g.N, nr, n1, nullptr, g.counts[i], nullptr,
+                                  st, kExplicitBest, false);
+      HIP_CHECK(hipFreeAsync(buf, st));
+    }
+  }
+  for (CkGroup& g : gs)
+    if (g.ws) {
+      HIP_CHECK(hipFreeAsync(g.ws, st));
+      g.ws = nullptr;
+    }
+  // (the redo counts of the last call, for cvd_chunk_stats)
+  int64_t tot = 0;
+  for (auto& v : rn)
+    for (int32_t c : v) tot += c;
+  cvd::ck_last[3] = tot;
+  return rc;
 }
 
 int cvd::upload_model(cvd_model& M, int device) {
@@ -2028,7 +2263,6 @@ int cvd::upload_model(cvd_model& M, int device) {
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (hipFunction_t)M.rtc_fn, M.rtc_block,
                                                            rtc_dyn_lds(M)) == hipSuccess &&
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && nb > 0 && ncu > 0) {
-      HIP_CHECK(hipMalloc((void**)&M.d_wq, kWqRing * sizeof(uint32_t)));
       M.rtc_persist_grid = (int64_t)nb * ncu;
     }
   }
@@ -2041,12 +2275,12 @@ void cvd::free_model_device(cvd_model& M) {
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
   void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_filt_lds, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
-                  M.d_bmk1, M.d_bfly, M.d_err, M.d_bfilt, M.d_bfilt_lds, M.d_bkey, M.d_bdkey, M.d_bpf, M.d_wq};
+                  M.d_bmk1, M.d_bfly, M.d_err, M.d_bfilt, M.d_bfilt_lds, M.d_bkey, M.d_bdkey, M.d_bpf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
   M.d_filt = nullptr; M.d_filt_lds = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_t2 = nullptr;
-  M.d_bfilt = nullptr; M.d_bfilt_lds = nullptr; M.d_bkey = nullptr; M.d_bdkey = nullptr; M.d_bpf = nullptr; M.d_wq = nullptr;
+  M.d_bfilt = nullptr; M.d_bfilt_lds = nullptr; M.d_bkey = nullptr; M.d_bdkey = nullptr; M.d_bpf = nullptr;
   M.rtc_persist_grid = 0;
   M.rtc_bs = false;
   M.rtc_pf = false;
@@ -2100,8 +2334,17 @@ extern "C" int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, do
                          random_input, seq_base, seq_stride, d_r, pitch, q0, count, stream);
 }
 
+static int detect_one(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq, int64_t n_h1,
+                      double* d_sums, int64_t* d_counts, int32_t path, void* stream);
+
 extern "C" int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
                           int64_t n_h1, double* d_sums, int64_t* d_counts, int32_t path, void* stream) {
+  cvd::ck_last = {0, 0, 0, 0};
+  return detect_one(model, d_r, N, nseq, n_h1, d_sums, d_counts, path, stream);
+}
+
+static int detect_one(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq, int64_t n_h1,
+                      double* d_sums, int64_t* d_counts, int32_t path, void* stream) {
   if (!model || (!d_r && N > 0 && nseq > 0) || !d_counts || N < 0 || nseq < 0 || n_h1 < 0 || n_h1 > nseq) {
     set_error("bad detect arguments");
     return CVD_E_INVALID;
@@ -2117,6 +2360,17 @@ extern "C" int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N
   if (path == CVD_PATH_AUTO) path = model->kind == 0 ? CVD_PATH_TABLE : CVD_PATH_EXPLICIT;
   if (path == CVD_PATH_TABLE)
     return launch_detect_table(*model, d_r, N, nseq, n_h1, d_sums, d_counts, stream, early);
+  // counts of a batch too small to fill the device: the chunked launch (same counts)
+  CkPlan P;
+  if (path == CVD_PATH_EXPLICIT && !d_sums && !early && model->kind == 1 && ck_plan(*model, N, nseq, &P)) {
+    std::vector<CkGroup> gs(1);
+    CkGroup& g = gs[0];
+    g.m = {model}; g.r = {d_r}; g.nseq = {nseq}; g.nh1 = {n_h1}; g.counts = {d_counts}; g.P = P; g.N = N;
+    cvd::ck_last = {cvd::ck_last[0] + 1, P.C, P.L, 0};
+    rc = ck_submit(g, (hipStream_t)stream);
+    if (rc) return rc;
+    return ck_finish(gs, (hipStream_t)stream);
+  }
   if (path == CVD_PATH_EXPLICIT || path == CVD_PATH_EXPLICIT_GENERIC || path == CVD_PATH_EXPLICIT_ORBIT ||
       path == CVD_PATH_EXPLICIT_BUTTERFLY)
     return launch_detect_explicit(*model, d_r, N, nseq, n_h1, d_sums, d_counts, nullptr, stream,
@@ -2176,6 +2430,11 @@ extern "C" int cvd_detect_multi(const cvd_model* const* models, int32_t nm, cons
   // the work queue keeps a CU's waves busy to the end, which a merged block launch does not
   // (cvd_model_info.persist_seqs)
   auto merges = [&](int32_t k) { return multi_ok(*models[k]) && persist_grid(*models[k], nseq[k]) == 0; };
+  // groups of batches too small to fill the device: chunked launches (same counts), their
+  // decisions and reruns after the last launch of the call (ck_finish)
+  std::vector<CkGroup> ck;
+  const bool ck_ok = (base == CVD_PATH_AUTO || base == CVD_PATH_EXPLICIT) && !early;
+  cvd::ck_last = {0, 0, 0, 0};
   while (i < nm) {
     const cvd_model& M = *models[i];
     const bool mok = (base == CVD_PATH_AUTO || base == CVD_PATH_EXPLICIT) && merges(i);
@@ -2183,16 +2442,41 @@ extern "C" int cvd_detect_multi(const cvd_model* const* models, int32_t nm, cons
     if (mok)
       while (j < nm && j - i < kMultiMax && merges(j) && multi_same(M, *models[j])) ++j;
     int rc;
+    bool sums_any = false;
+    int64_t ntot = 0;
+    for (int32_t x = i; x < (mok ? j : i + 1); ++x) {
+      sums_any = sums_any || (d_sums && d_sums[x]);
+      ntot += nseq[x];
+    }
+    CkPlan P;
+    if (ck_ok && !sums_any && M.kind == 1 && (mok || j == i + 1) && ck_plan(M, N, ntot, &P)) {
+      if (!mok) j = i + 1;
+      CkGroup g;
+      for (int32_t x = i; x < j; ++x) {
+        if (nseq[x] <= 0) continue;
+        g.m.push_back(models[x]); g.r.push_back(d_r[x]); g.nseq.push_back(nseq[x]); g.nh1.push_back(n_h1[x]);
+        g.counts.push_back(d_counts[x]);
+      }
+      g.P = P;
+      g.N = N;
+      if (!g.m.empty()) {
+        ck.push_back(std::move(g));
+        if ((rc = ck_submit(ck.back(), (hipStream_t)stream))) return rc;
+        cvd::ck_last = {cvd::ck_last[0] + 1, P.C, P.L, 0};
+      }
+      i = j;
+      continue;
+    }
     if (mok && j - i > 1) {
       rc = launch_multi(models, i, j, d_r, N, nseq, n_h1, d_sums, d_counts, stream, early);
     } else {
       j = i + 1;
-      rc = cvd_detect(models[i], d_r[i], N, nseq[i], n_h1[i], d_sums ? d_sums[i] : nullptr, d_counts[i], path, stream);
+      rc = detect_one(models[i], d_r[i], N, nseq[i], n_h1[i], d_sums ? d_sums[i] : nullptr, d_counts[i], path, stream);
     }
     if (rc) return rc;
     i = j;
   }
-  return CVD_OK;
+  return ck_finish(ck, (hipStream_t)stream);
 }
 
 extern "C" int cvd_trace(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
@@ -2310,6 +2594,12 @@ extern "C" int cvd_mc_fused(const cvd_model* model, const cvd_code* enc1, const 
   if ((rc = check_device(*model))) return rc;
   return mc_fused_sliced(*model, e1, e2, seed, grid_tag(N, p), noise_threshold(p), N, trial_begin, trial_end, d_sums,
                          d_counts, stream, early);
+}
+
+extern "C" int cvd_chunk_last(int64_t* out4) {
+  if (!out4) { set_error("null argument"); return CVD_E_INVALID; }
+  for (int i = 0; i < 4; ++i) out4[i] = cvd::ck_last[i];
+  return CVD_OK;
 }
 
 extern "C" int cvd_model_device_error(cvd_model* model, int32_t* flags_out) {

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CVD_ABI_VERSION 10
+#define CVD_ABI_VERSION 11
 
 #define CVD_OK 0
 #define CVD_E_INVALID -1      /* bad argument */
@@ -219,9 +219,18 @@ int cvd_generate(const cvd_code* enc, uint64_t seed, uint32_t tag, double p, int
  * successes, d_counts[1] += H2 successes (int64, accumulated, not cleared).
  * d_sums (nullable): [nseq][2] doubles.
  * A launch of the bit-sliced kernel past cvd_model_info.persist_seqs is persistent: its
- * waves take their sequences from a work-queue counter, one of a ring of 64 per model that
- * the call zeroes on `stream`; at most 64 such launches of one model may be in flight at
- * once (across streams). */
+ * waves take their sequences from a work-queue counter the call allocates, zeroes and frees
+ * on `stream` (stream-ordered, so launches on any number of streams never share one).
+ * Chunked launches (counts only: d_sums NULL, no early decision; the bit-sliced kernel): a
+ * batch too small to fill the device twice -- the reference's own call shape, e.g. 10,000
+ * trials per p -- has every sequence's N steps cut into C time chunks of L steps, each
+ * started on a lane of its own W steps early from D = 0 and kept only where the chunks
+ * join (D at a chunk's start equals the previous chunk's D at its end) and the decision is
+ * certain under the rounding bounds of both summation orders; every other sequence is rerun
+ * on the sequential kernel, so the counts equal the unchunked launch's exactly.  Such a
+ * call synchronises `stream` once (the rerun list).  CVD_CHUNK=0 disables it, =1 forces it
+ * wherever C >= 2; CVD_CHUNK_WARM (1152 steps) and CVD_CHUNK_UNITS set W and the target lane
+ * count. */
 int cvd_detect(const cvd_model* model, const uint32_t* d_r, int64_t N, int64_t nseq,
                int64_t n_h1, double* d_sums, int64_t* d_counts, int32_t path, void* stream);
 
@@ -283,6 +292,12 @@ int cvd_mc_run_grid(const cvd_model* const* models, const cvd_code* enc1, const 
  * report it: a caller checks it once after its launches (the Python host does after
  * run_trials with sums, run_grid, detect_multi's callers, run_experiment and the bench). */
 int cvd_model_device_error(cvd_model* model, int32_t* flags_out);
+
+/* The chunked launches of this process's last cvd_detect / cvd_detect_multi call (cvd_mc_run
+ * and cvd_mc_run_grid make such calls per batch): out[0] chunked launch groups (0: none),
+ * out[1] chunks per sequence C, out[2] steps per chunk L, out[3] sequences the decisions
+ * left to the sequential rerun.  Diagnostic (tests, bench); not thread-safe. */
+int cvd_chunk_last(int64_t* out4);
 
 /* The same grid point in ONE kernel per launch, without streams in HBM: every lane
  * generates its own sequence's received words (cvd_generate's encoder and noise, bit

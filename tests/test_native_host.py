@@ -25,7 +25,7 @@ def test_lib_exports_every_header_symbol(pkg):
     assert len(names) >= 15
     for name in names:
         assert hasattr(lib, name), f"libcvd.so does not export {name}"
-    assert lib.cvd_version() == pkg._lib.ABI_VERSION == 10
+    assert lib.cvd_version() == pkg._lib.ABI_VERSION == 11
     assert set(names) <= set(pkg._lib.EXPORTS), "python binding misses a header function"
 
 
