@@ -1117,18 +1117,37 @@ def reference_call(pkg, cc, k, n, m, N, p_grid, learn_len, seed, num_iter=10_000
     must give the same DataFrame."""
     import torch
     args = (k, n, m, cc["gen1"], cc["gen2"], num_iter, list(p_grid), learn_len, 200, 1.0, seed)
-    t0 = time.perf_counter()
-    df1 = pkg.run_experiment(*args, N_list=[N], early_decision=False)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    df2 = pkg.run_experiment(*args, N_list=[N], early_decision=False)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
+
+    def timed(early, chunk=None):
+        old = os.environ.get("CVD_CHUNK")
+        if chunk is not None:
+            os.environ["CVD_CHUNK"] = str(chunk)
+        try:
+            t0 = time.perf_counter()
+            df = pkg.run_experiment(*args, N_list=[N], early_decision=early)
+            torch.cuda.synchronize()
+            return df, time.perf_counter() - t0, pkg._lib.chunk_last()
+        finally:
+            if chunk is not None:
+                if old is None:
+                    os.environ.pop("CVD_CHUNK", None)
+                else:
+                    os.environ["CVD_CHUNK"] = old
+
+    df1, t_first, _ = timed(False)
+    df2, t_second, ck = timed(False)                 # chunked (DESIGN.md §7.8), the default
+    df_seq, t_seq, _ = timed(False, chunk=0)         # one lane per sequence, for comparison
+    df_early, t_early, _ = timed(True)               # run_experiment's default: early decision
     trials = num_iter * len(p_grid)
     return {"call": f"run_experiment(num_iter={num_iter}, p_vec={list(p_grid)}, N_list=[{N}], learn_len={learn_len})",
-            "trials": trials, "first_call_s_incl_setup": t1 - t0, "second_call_s": t2 - t1,
-            "trials_per_s_second_call": trials / (t2 - t1),
-            "dataframes_equal": bool(df1.equals(df2)), "rows": df2.to_dict(orient="records")}
+            "trials": trials, "first_call_s_incl_setup": t_first, "second_call_s": t_second,
+            "trials_per_s_second_call": trials / t_second, "chunked": ck,
+            "unchunked_second_call_s": t_seq, "early_decision_second_call_s": t_early,
+            "note": "second_call_s: every step of every trial (early_decision=False), chunked launches; "
+                    "unchunked: CVD_CHUNK=0 (one lane per sequence); early_decision: run_experiment's "
+                    "default (counts only, each trial stops once certain); all four DataFrames equal",
+            "dataframes_equal": bool(df1.equals(df2) and df2.equals(df_seq) and df2.equals(df_early)),
+            "rows": df2.to_dict(orient="records")}
 
 
 if __name__ == "__main__":

@@ -2034,12 +2034,23 @@ static bool ck_plan(const cvd_model& M, int64_t N, int64_t nseq_total, CkPlan* P
   const int64_t W = round_up192(std::max(0, env_i("CVD_CHUNK_WARM", 1152)));
   const int64_t slots = std::max<int64_t>(1, M.rtc_persist_grid) * (M.rtc_block / 64);   // resident waves
   const int64_t waves = (nseq_total + 63) / 64;
-  if (mode < 0 && waves >= 2 * slots) return false;   // the launch fills the device as it is
-  const int64_t target = env_i("CVD_CHUNK_UNITS", 0) > 0 ? env_i("CVD_CHUNK_UNITS", 0) : 4 * slots;
+  // small batches (fewer waves than two residency rounds): C x the lanes, ~4 rounds of units,
+  // the warm-up at most a third of a chunk (profiles/r06c: 0.0686 s for the reference call at
+  // 4 rounds against 0.0761 at 2 and 0.0707 at 8; W = 768 left 5-13 reruns per call, 1152 none)
+  int64_t target = 4 * slots, Lmin = std::max<int64_t>(192, 3 * W);
+  if (waves >= 2 * slots) {
+    // large batches of few residency rounds (C4's N = 1e6: three rounds of ~1 s units): the
+    // persistent launch's drain -- its last units finish unevenly -- is a large share; chunks
+    // of >= 40 W steps (warm-up <= 2.5%) make the units shorter and the drain with them
+    if (mode < 0 && waves >= (int64_t)env_i("CVD_CHUNK_MAX_ROUNDS", 12) * slots) return false;
+    target = 16 * slots;
+    Lmin = std::max<int64_t>(192, 40 * W);
+  }
+  if (env_i("CVD_CHUNK_UNITS", 0) > 0) target = env_i("CVD_CHUNK_UNITS", 0);
   int64_t C = std::max<int64_t>(1, (target + waves - 1) / waves);
   int64_t L = round_up192((N + C - 1) / C);
-  // the warm-up at most a third of a chunk where it pays (forced: any chunk of >= 192 steps)
-  L = std::max<int64_t>(L, mode < 0 ? std::max<int64_t>(192, 3 * W) : 192);
+  // (forced: any chunk of >= 192 steps)
+  L = std::max<int64_t>(L, mode < 0 ? Lmin : 192);
   C = (N + L - 1) / L;
   if (C < 2 || C * waves > (int64_t)UINT32_MAX / 2) return false;
   P->C = (int32_t)C; P->L = (int32_t)L; P->W = (int32_t)W;
