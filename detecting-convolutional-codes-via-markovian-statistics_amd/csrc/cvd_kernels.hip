@@ -1874,7 +1874,9 @@ bool cvd::walk_preferred(const cvd_model& M, bool early) {
   // the bit-sliced kernel's lockstep steps are cheaper, so it walks only below 1/20: p = 0.02
   // (70,134 rows / 10^6) runs 1,584 ms lockstep against 1,703 walking, p = 0.01 (29,626) 1,433
   // walking against 1,534 (profiles/r05r_p*/)
-  const int64_t ratio = bitslice_preferred(M) ? 20 : 10;
+  // (keyed on the kernel that runs once the JIT has decided -- a model whose bit-sliced build
+  // failed runs the butterfly kernel, ADVICE r05 -- else on the tables' prediction)
+  const int64_t ratio = (M.rtc_fn ? M.rtc_bs : bitslice_preferred(M)) ? 20 : 10;
   return !early && M.kind == 1 && M.learn_len_eff > 0 && ratio * M.n_rows < M.learn_len_eff;
 }
 

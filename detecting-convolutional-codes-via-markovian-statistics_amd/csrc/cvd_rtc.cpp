@@ -26,6 +26,7 @@
 #include <hip/hiprtc.h>
 #include <fcntl.h>
 #include <spawn.h>
+#include <sys/file.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -298,6 +299,23 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
     if (fn_multi_out) *fn_multi_out = (void*)fnm;
     return 0;
   };
+  // Ranks that start together (one process per GPU, the same decoder) compile a variant once:
+  // the first takes an exclusive lock on the cache entry, compiles and publishes it; the others
+  // wait for the lock and load the published object (8 concurrent compiles made
+  // every rank's setup 22.5 s).  The lock is released when `lk` closes.
+  struct Lock {
+    int fd = -1;
+    ~Lock() {
+      if (fd >= 0) ::close(fd);   // (closing drops the flock)
+    }
+  } lk;
+  if (!cpath.empty() && std::getenv("CVD_JIT_NOLOCK") == nullptr) {
+    lk.fd = ::open((cpath + ".lock").c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+    if (lk.fd >= 0 && ::flock(lk.fd, LOCK_EX) != 0) {
+      ::close(lk.fd);
+      lk.fd = -1;
+    }
+  }
   if (!cpath.empty() && cache_load(cpath, code)) {
     if (load(fn, fnm)) return done();
     ::unlink(cpath.c_str());   // unusable cached object: rebuild it

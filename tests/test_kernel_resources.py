@@ -18,6 +18,9 @@ SPEC = os.path.join(ROOT, "detecting-convolutional-codes-via-markovian-statistic
 
 VARIANTS = {
     "butterfly": [],
+    # the butterfly kernel on a walking model's 128-KiB LDS filter in 1,024-thread blocks: what
+    # a model sized for k1s runs if its bit-sliced JIT build fails
+    "butterfly_ldsf_1024": ["-DCVD_K1B_LDSF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10"],
     "k1s_pf": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1S_PF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10"],
     "k1s_ldsf": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1B_LDSF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10"],
     "k1s_global": ["-DCVD_K1B_BITSLICE=1"],
