@@ -112,6 +112,8 @@ EXPORTS = {
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     "cvd_model_device_error": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
     "cvd_chunk_last": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int64)]),
+    "cvd_jit_prebuild": (ctypes.c_int, [ctypes.POINTER(cvd_code), ctypes.c_char_p, ctypes.c_char_p,
+                                        ctypes.POINTER(ctypes.c_int32)]),
     "cvd_mc_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cvd_code), ctypes.POINTER(cvd_code),
                                     ctypes.c_double, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64,
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,

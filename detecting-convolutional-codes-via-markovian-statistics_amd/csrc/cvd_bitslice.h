@@ -247,12 +247,24 @@ CVD_HD void bs_canon(bs_u32& lo, bs_u32& hi) {
 // ─────────────────────── host: images, digest, key hash ───────────────────────
 // planes of D (64 metric bytes, canonical state order) at phase ph: out[4 r + i] = plane i
 // of word r
+// (host: the model's table build; bs_addr of every (phase, state) once)
+struct BsAddrTab {
+  unsigned char a[6][64];
+};
+inline BsAddrTab bs_addr_tab() {
+  BsAddrTab t;
+  for (int ph = 0; ph < 6; ++ph)
+    for (int s = 0; s < 64; ++s) t.a[ph][s] = (unsigned char)bs_addr(s, ph);
+  return t;
+}
 inline void bs_image(const unsigned char* D, int ph, bs_u32 out[8]) {
+  static const BsAddrTab tab = bs_addr_tab();
   for (int i = 0; i < 8; ++i) out[i] = 0u;
   for (int s = 0; s < 64; ++s) {
-    const int A = bs_addr(s, ph);
-    for (int i = 0; i < 4; ++i)
-      if ((D[s] >> i) & 1) out[4 * (A >> 5) + i] |= 1u << (A & 31);
+    const int A = tab.a[ph][s];
+    bs_u32* o = out + 4 * (A >> 5);
+    const bs_u32 d = D[s];
+    for (int i = 0; i < 4; ++i) o[i] |= ((d >> i) & 1u) << (A & 31);
   }
 }
 // the phase-0 digest plane z = bit0(D) ^ bit1(D)

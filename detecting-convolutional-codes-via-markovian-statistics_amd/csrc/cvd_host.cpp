@@ -475,11 +475,12 @@ void build_hash(cvd_model& Mo) {
   //    learned rows reads without hashing (table mode): the rows a walk visits
   //    sit together in first-visit order instead of scattered over the
   //    directory (load <= 1/16).
+  PhaseTimer pt;
   const int m = Mo.dec.m, M = 1 << m, R = 1 << Mo.dec.n, nw = nib_words(m);
   Mo.h_rsw = row_words(Mo.dec.n);
   // Key and record of a slot in one power-of-two slot (128 B at m = 6, n = 2): a
   // hit reads one line instead of a key line and a record line (p = 0.1 launch
-  // 3,122 -> 2,969 ms, profiles/r02z5_il/).  h_row stays empty and the device
+  // 3,122 -> 2,969 ms, profiles/r02z5_il/).  h_row_rows stays empty and the device
   // record base is the key base + nw dwords.  CVD_SLOT_IL=0: separate key and
   // record arrays (timing studies).
   const char* il = std::getenv("CVD_SLOT_IL");
@@ -524,10 +525,12 @@ void build_hash(cvd_model& Mo) {
   Mo.h_filt.assign((size_t)fcap, 0u);
   Mo.h_filt_lds.assign(ldsf ? (size_t)fcap : 0u, 0u);
   const unsigned npat = (unsigned)kFilterPatterns;   // the kernels' pattern table (cvd_keys.h)
-  Mo.h_key.assign((size_t)cap * ssw, kEmptyKey);
-  Mo.h_row.assign(interleave ? 0 : (size_t)cap * Mo.h_rsw, 0u);
+  Mo.h_key_rows.assign((size_t)Mo.n_rows * ssw, kEmptyKey);
+  Mo.h_key_slot.assign((size_t)Mo.n_rows, 0u);
+  Mo.h_row_rows.assign(interleave ? 0 : (size_t)Mo.n_rows * Mo.h_rsw, 0u);
   Mo.h_drow.assign((size_t)Mo.n_rows * Mo.h_rsw, 0u);
   Mo.max_probe = 0;
+  pt.mark("  nibble tables: allocate");
   // Device row ids (drow index, successor fields, slot0): rows by descending visit count
   // of the learning chain, which is the trial streams' own process (encoder G1, BSC(p)),
   // so the rows table walks read most sit together in few cache lines instead of in
@@ -555,6 +558,7 @@ void build_hash(cvd_model& Mo) {
       for (int w = 0; w < nw; ++w) kw[w] = key_swap(kw[w]);   // device key layout
     key_hash(kw, nw, phs[(size_t)i], pls[(size_t)i]);
   });
+  std::vector<uint8_t> occupied((size_t)cap, 0);
   for (int64_t i = 0; i < Mo.n_rows; ++i) {
     const uint32_t* kw = kws.data() + (size_t)i * nw;
     const uint32_t ph = phs[(size_t)i], pl = pls[(size_t)i];
@@ -568,11 +572,14 @@ void build_hash(cvd_model& Mo) {
     }
     uint64_t slot = ph & (uint64_t)(cap - 1);
     int probe = 0;
-    while (Mo.h_key[slot * ssw] != kEmptyKey) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
+    while (occupied[slot]) { slot = (slot + 1) & (uint64_t)(cap - 1); ++probe; }
+    occupied[slot] = 1;
     Mo.max_probe = std::max(Mo.max_probe, probe);
-    for (int w = 0; w < nw; ++w) Mo.h_key[slot * ssw + w] = kw[w];
+    for (int w = 0; w < nw; ++w) Mo.h_key_rows[(size_t)i * ssw + w] = kw[w];
+    Mo.h_key_slot[(size_t)i] = (uint32_t)slot;
     slot_of[(size_t)i] = (int64_t)slot;
   }
+  pt.mark("  nibble tables: hash + insert");
   // row keys by device row id (the walk mode of the specialised kernel rebuilds a
   // lane's metric vector from the key of the last row it walked)
   Mo.h_dkey.assign((size_t)Mo.n_rows * nw, 0u);
@@ -596,11 +603,12 @@ void build_hash(cvd_model& Mo) {
     }
     std::memcpy(Mo.h_dkey.data() + (size_t)dev_of[(size_t)i] * nw, kws.data() + (size_t)i * nw,
                 sizeof(uint32_t) * (size_t)nw);
-    uint32_t* hw = interleave ? Mo.h_key.data() + (size_t)slot_of[(size_t)i] * ssw + nw
-                              : Mo.h_row.data() + (size_t)slot_of[(size_t)i] * Mo.h_rsw;
+    uint32_t* hw = interleave ? Mo.h_key_rows.data() + (size_t)i * ssw + nw
+                              : Mo.h_row_rows.data() + (size_t)i * Mo.h_rsw;
     std::memcpy(hw, dw, sizeof(uint32_t) * Mo.h_rsw);
   });
   Mo.slot0 = (int32_t)dev_of[0];   // D_0 = 0 is row 0 in both model kinds
+  pt.mark("  nibble tables: records");
   // Bit-sliced tables of the m = 6 kernel k1s (cvd_bitslice.h): the same rows and records,
   // found by the hash of the canonical digest plane z = bit0(D) ^ bit1(D) (one filter entry
   // per row whatever the lane's layout phase); a directory slot holds the row's image at
@@ -615,7 +623,8 @@ void build_hash(cvd_model& Mo) {
   // the kernel addresses the directory, the two-step records and the images by 32-bit byte
   // offsets: past 4 GiB (over ~2·10^6 rows) the model keeps the nibble tables
   if (bcap * 256 > ((int64_t)1 << 32) || Mo.n_rows * 512 > ((int64_t)1 << 32)) Mo.bs = false;
-  Mo.h_bfilt.clear(); Mo.h_bfilt_lds.clear(); Mo.h_bkey.clear(); Mo.h_bdkey.clear(); Mo.h_bpf.clear();
+  Mo.h_bfilt.clear(); Mo.h_bfilt_lds.clear(); Mo.h_bkey_rows.clear(); Mo.h_bkey_slot.clear(); Mo.h_bdkey.clear();
+  Mo.h_bpf.clear();
   Mo.bhcap = 0; Mo.bmax_probe = 0;
   if (Mo.bs) {
     // the filter's pattern table (kernel LDS: 8 B per pattern pair); CVD_BS_PAT_BITS 8..12
@@ -633,10 +642,12 @@ void build_hash(cvd_model& Mo) {
     const unsigned bnpat = 1u << Mo.bs_pat_bits;
     Mo.bhcap = bcap;
     constexpr int kSlotW = 64, kRecW = 48, kImgW = 48;
-    Mo.h_bkey.assign((size_t)bcap * kSlotW, 0u);   // c = 0 in every record: empty
+    Mo.h_bkey_rows.assign((size_t)Mo.n_rows * kSlotW, 0u);   // (the empty slots: zero, c = 0 in every record)
+    Mo.h_bkey_slot.assign((size_t)Mo.n_rows, 0u);
     Mo.h_bfilt.assign((size_t)fcap, 0u);
     Mo.h_bfilt_lds.assign(ldsf ? (size_t)fcap : 0u, 0u);
     Mo.h_bdkey.assign((size_t)Mo.n_rows * kImgW, 0u);
+    pt.mark("  bit-sliced tables: allocate");
     std::vector<uint32_t> bph((size_t)Mo.n_rows), bpl((size_t)Mo.n_rows);
     parallel_for(Mo.n_rows, [&](int64_t i, int) {
       uint32_t z[2];
@@ -644,7 +655,6 @@ void build_hash(cvd_model& Mo) {
       bs_key_hash(z[0], z[1], bph[(size_t)i], bpl[(size_t)i]);
     });
     std::vector<uint8_t> used((size_t)bcap, 0);
-    std::vector<int64_t> bslot((size_t)Mo.n_rows);
     for (int64_t i = 0; i < Mo.n_rows; ++i) {
       const uint32_t ph = bph[(size_t)i], pl = bpl[(size_t)i];
       const size_t fb = (size_t)filter_block_index(pl, (uint32_t)(fcap / 2 - 1));
@@ -664,10 +674,11 @@ void build_hash(cvd_model& Mo) {
       while (used[slot]) { slot = (slot + 1) & (uint64_t)(bcap - 1); ++probe; }
       used[slot] = 1;
       Mo.bmax_probe = std::max(Mo.bmax_probe, probe);
-      bslot[(size_t)i] = (int64_t)slot;
+      Mo.h_bkey_slot[(size_t)i] = (uint32_t)slot;
     }
+    pt.mark("  bit-sliced tables: hash + insert");
     parallel_for(Mo.n_rows, [&](int64_t i, int) {
-      uint32_t* sp = Mo.h_bkey.data() + (size_t)bslot[(size_t)i] * kSlotW;
+      uint32_t* sp = Mo.h_bkey_rows.data() + (size_t)i * kSlotW;
       uint32_t* dk = Mo.h_bdkey.data() + (size_t)dev_of[(size_t)i] * kImgW;
       for (int ph = 0; ph < 6; ++ph) {
         bs_image(Mo.keys.data() + (size_t)i * M, ph, sp + 8 * ph);
@@ -676,6 +687,7 @@ void build_hash(cvd_model& Mo) {
       std::memcpy(sp + kRecW, Mo.h_drow.data() + (size_t)dev_of[(size_t)i] * Mo.h_rsw, sizeof(uint32_t) * 16);
     });
   }
+  pt.mark("  bit-sliced tables: images + records");
   // two-step walk records (k1b_walk), for models that walk: per device row d and word pair
   // (r1, r2), 32 B {log P̂1(d, r1), log P̂1(d1, r2), (d1 + 1) | c(d, r1) << 28,
   // (d2 + 1) | c(d1, r2) << 28}, d1 / d2 the rows after one / two steps (0 = not a row)
@@ -857,17 +869,18 @@ int model_create(const cvd_code* dec, const cvd_learn_params* prm, int device, v
   static std::map<std::tuple<int, int, int, std::vector<uint32_t>>, int64_t> bfs_too_big;   // -> largest cap tried
   const auto ckey = std::make_tuple(T.m, T.k, T.n,
                                     std::vector<uint32_t>(Mo->dec.gmask, Mo->dec.gmask + T.n * T.k));
-  bool known_big = false;
+  // (the lock is held over the BFS: models of one code built on several threads at once --
+  // Detector.prepare_models -- wait for the first thread's verdict instead of each running the
+  // capped BFS, 0.2-0.5 s of CPU per model of the m = 6 code)
   {
     std::lock_guard<std::mutex> lk(bfs_mu);
     auto it = bfs_too_big.find(ckey);
-    known_big = it != bfs_too_big.end() && it->second >= cap;
-  }
-  rc = (cap > 0 && !known_big) ? bfs(T, cap, states, next, S) : CVD_E_CAPACITY;
-  if (rc == CVD_E_CAPACITY && cap > 0 && !known_big) {
-    std::lock_guard<std::mutex> lk(bfs_mu);
-    int64_t& c = bfs_too_big[ckey];
-    c = std::max(c, cap);
+    const bool known_big = it != bfs_too_big.end() && it->second >= cap;
+    rc = (cap > 0 && !known_big) ? bfs(T, cap, states, next, S) : CVD_E_CAPACITY;
+    if (rc == CVD_E_CAPACITY && cap > 0 && !known_big) {
+      int64_t& c = bfs_too_big[ckey];
+      c = std::max(c, cap);
+    }
   }
   pt.mark("bfs");
   std::unordered_map<int64_t, double> memo;
@@ -1183,6 +1196,42 @@ extern "C" int cvd_model_create_device(const cvd_code* dec, const cvd_learn_para
     stats_out[6] = st.sequential_seconds;
   }
   return rc;
+}
+
+// The code-specialised kernel's default variants for a decoder, compiled now (no device
+// needed) into `dir`, the prebuilt cache the run-time compile looks in first (cvd_rtc.cpp): a
+// fresh box then loads them instead of compiling ~10 s per variant at model upload.  The
+// bit-sliced codes' (m = 6) lockstep variant (pre-filter, 1,024-thread blocks) and the walking
+// models' LDS-filter variants (1,024 and 512 threads).
+extern "C" int cvd_jit_prebuild(const cvd_code* dec, const char* arch, const char* dir, int32_t* n_built) {
+  CVD_TRY
+  if (!dec || !arch || !dir || !n_built) { set_error("null argument"); return CVD_E_INVALID; }
+  *n_built = 0;
+  cvd_model Mo;
+  int rc = parse_code(dec, Mo.dec);
+  if (rc) return rc;
+  const Tabs T = make_tabs(Mo.dec);
+  build_bmp(Mo, T);
+  if (!Mo.k1b_ok || !bitslice_preferred(Mo)) return CVD_OK;   // (only the bit-sliced codes)
+  const std::string vs[] = {
+      rtc_variant_defs(kBsPfLog2Bits >= 20 ? 1024 : 512, false, kFilterPatBitsLds, true, true, kBsPfLog2Bits),
+      rtc_variant_defs(1024, true, kFilterPatBitsLds, true, false, kBsPfLog2Bits),
+      rtc_variant_defs(512, true, kFilterPatBitsLds, true, false, kBsPfLog2Bits)};
+  std::vector<std::thread> th;
+  std::vector<int> res(3, 0);
+  std::vector<std::string> errs(3);
+  for (int i = 0; i < 3; ++i)
+    th.emplace_back([&, i] {
+      res[i] = rtc_prebuild(Mo.dec.m, Mo.bfly_x, vs[i].c_str(), arch, dir);
+      if (res[i]) errs[i] = last_error_copy();
+    });
+  for (auto& t : th) t.join();
+  for (int i = 0; i < 3; ++i) {
+    if (res[i]) { set_error(errs[i]); return CVD_E_UNSUPPORTED; }
+    ++*n_built;
+  }
+  return CVD_OK;
+  CVD_CATCH
 }
 
 extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {

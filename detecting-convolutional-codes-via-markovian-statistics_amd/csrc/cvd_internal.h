@@ -38,10 +38,18 @@ struct cvd_model {
   std::vector<uint32_t> h_filt;   // [fcap] blocked Bloom filter words (filter_pattern)
   std::vector<uint32_t> h_filt_lds;   // the same filter with 2^kFilterPatBitsLds patterns (LDS kernel), or empty
   int64_t fcap = 0;               // filter words, power of two
-  std::vector<uint32_t> h_key;    // [hcap][NW] nibble-packed metric vector, word 0 = kEmptyKey if empty
+  // The directories are kept on the host as their occupied slots only -- the slot index of
+  // every row and the row's slot contents, by row -- and expanded on the device at upload
+  // (every other slot empty; cvd_kernels.hip upload_model): a 1e6-row model's 2 GiB + 2 GiB of
+  // mostly empty slots are never built, zeroed or copied on the host.
+  std::vector<uint32_t> h_key_rows;   // [n_rows][h_ssw]: slot contents, nibble-packed metric vector (and,
+                                      // interleaved, its record at dword NW); empty slots: kEmptyKey words
+  std::vector<uint32_t> h_key_slot;   // [n_rows]: the row's directory slot (< hcap)
   int32_t h_rsw = 0;              // row record stride in dwords (row_words)
   int32_t h_ssw = 0;              // directory slot stride in dwords: nw, or (CVD_SLOT_IL) key + record in one slot
-  std::vector<uint32_t> h_row;    // [hcap][h_rsw]: per r, 16 B {log P̂1[r] (f64), successor row[r] (i32, -1: none), 0}
+  std::vector<uint32_t> h_row_rows;   // (CVD_SLOT_IL=0) [n_rows][h_rsw] records at the key slot's index of
+                                      // a separate [hcap][h_rsw] array: per r, 16 B {log P̂1[r] (f64),
+                                      // successor row[r] (i32, -1: none), 0}; empty slots zero
   std::vector<uint32_t> h_drow;   // [n_rows][h_rsw]: the same records dense by row id (table mode),
                                   // dword 3 of entry r = the T_ref count c(r)
   std::vector<uint32_t> h_dkey;   // [n_rows][NW]: row keys (device layout) by device row id
@@ -55,7 +63,9 @@ struct cvd_model {
   int64_t bhcap = 0;
   int32_t bmax_probe = 0;
   std::vector<uint32_t> h_bfilt, h_bfilt_lds;   // [fcap] each (the LDS copy only with h_filt_lds)
-  std::vector<uint32_t> h_bkey;   // [bhcap][64]: images 8 words x 6 phases, records 4 x 4 (c = 0: empty)
+  std::vector<uint32_t> h_bkey_rows;   // [n_rows][64]: slot contents -- images 8 words x 6 phases,
+                                       // records 4 x 4 -- of the [bhcap][64] directory (empty: zero, c = 0)
+  std::vector<uint32_t> h_bkey_slot;   // [n_rows]: the row's slot (< bhcap)
   std::vector<uint32_t> h_bdkey;  // [n_rows][48]
   // LDS pre-filter of k1s (CVD_K1S_PF): one bit per row at bit pl >> (32 - kBsPfLog2Bits) of
   // its digest hash, 2^kBsPfLog2Bits bits (128 KiB) that a 1,024-thread block keeps in LDS;
@@ -161,6 +171,12 @@ int explicit_kernel_of(const cvd_model& M);
 int check_device(const cvd_model& M);
 int rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, void** fn_out,
                      void** fn_multi_out = nullptr);
+// the -D set of a specialised-kernel variant (upload_model, and cvd_jit_prebuild: the same text
+// keys the same code object)
+std::string rtc_variant_defs(int block, bool ldsf, int patbits, bool bs, bool pf, int pf_log2);
+// compile one variant for `arch` into `dir` (the prebuilt cache rtc_k1b_function reads first);
+// 0 = ok (or already there)
+int rtc_prebuild(int m, uint64_t xm, const char* variant_defs, const char* arch, const char* dir);
 void free_model_device(cvd_model& M);
 bool explicit_supported(int m, int k, int n);
 // the model gets the bit-sliced tables and kernel (m = 6 standard-butterfly codes;

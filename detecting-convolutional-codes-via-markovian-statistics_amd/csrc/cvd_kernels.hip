@@ -1559,6 +1559,37 @@ int dev_copy(T*& d, const std::vector<T>& h) {
   return CVD_OK;
 }
 
+// A directory from its occupied slots (cvd_internal.h h_key_rows / h_bkey_rows): every slot
+// `fill`, then row i's w dwords at slot slots[i].
+__global__ __launch_bounds__(kBlock) void dir_scatter_kernel(const uint32_t* rows, const uint32_t* slots, int64_t n,
+                                                             int32_t w, uint32_t* dir) {
+  const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (idx >= n * w) return;
+  const int64_t i = idx / w, k = idx - i * w;
+  dir[(size_t)slots[i] * (size_t)w + (size_t)k] = rows[idx];
+}
+
+int dev_directory(uint32_t*& d, const std::vector<uint32_t>& rows, const std::vector<uint32_t>& slots, int64_t cap,
+                  int32_t w, uint32_t fill) {
+  if (rows.empty() || cap <= 0) return CVD_OK;
+  const int64_t n = (int64_t)slots.size();
+  if ((int64_t)rows.size() != n * w) { set_error("directory rows / slots mismatch"); return CVD_E_INVALID; }
+  HIP_CHECK(hipMalloc(&d, (size_t)cap * (size_t)w * sizeof(uint32_t)));
+  HIP_CHECK(hipMemsetD32(d, (int)fill, (size_t)cap * (size_t)w));
+  uint32_t *dr = nullptr, *ds = nullptr;
+  HIP_CHECK(hipMalloc(&dr, rows.size() * sizeof(uint32_t)));
+  HIP_CHECK(hipMalloc(&ds, slots.size() * sizeof(uint32_t)));
+  HIP_CHECK(hipMemcpy(dr, rows.data(), rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(ds, slots.data(), slots.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  const unsigned grid = (unsigned)((n * w + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(dir_scatter_kernel, dim3(grid), dim3(kBlock), 0, 0, dr, ds, n, w, d);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipFree(dr));
+  HIP_CHECK(hipFree(ds));
+  return CVD_OK;
+}
+
 }  // namespace
 
 // ───────────────────────────── launchers ─────────────────────────────────────
@@ -2189,6 +2220,13 @@ static int ck_finish(std::vector<CkGroup>& gs, hipStream_t st) {
   return rc;
 }
 
+std::string cvd::rtc_variant_defs(int block, bool ldsf, int patbits, bool bs, bool pf, int pf_log2) {
+  return "-DCVD_K1B_BLOCK=" + std::to_string(block) + (ldsf ? " -DCVD_K1B_LDSF=1" : "") +
+         (patbits != kFilterPatBits ? " -DCVD_FILTER_PAT_BITS=" + std::to_string(patbits) : "") +
+         (bs ? " -DCVD_K1B_BITSLICE=1" : "") + (pf ? " -DCVD_K1S_PF=1" : "") +
+         (pf && pf_log2 != kBsPfLog2Bits ? " -DCVD_K1S_PF_LOG2=" + std::to_string(pf_log2) : "");
+}
+
 int cvd::upload_model(cvd_model& M, int device) {
   if (M.device == device) return CVD_OK;
   if (M.device >= 0) free_model_device(M);
@@ -2209,14 +2247,14 @@ int cvd::upload_model(cvd_model& M, int device) {
   if (M.hcap > 0) {
     if ((rc = dev_copy(M.d_filt, M.h_filt))) return rc;
     if ((rc = dev_copy(M.d_filt_lds, M.h_filt_lds))) return rc;
-    if ((rc = dev_copy(M.d_hkey, M.h_key))) return rc;
-    if ((rc = dev_copy(M.d_hrow, M.h_row))) return rc;
+    if ((rc = dev_directory(M.d_hkey, M.h_key_rows, M.h_key_slot, M.hcap, M.h_ssw, kEmptyKey))) return rc;
+    if ((rc = dev_directory(M.d_hrow, M.h_row_rows, M.h_key_slot, M.hcap, M.h_rsw, 0u))) return rc;
     if ((rc = dev_copy(M.d_drow, M.h_drow))) return rc;
     if ((rc = dev_copy(M.d_dkey, M.h_dkey))) return rc;
     if ((rc = dev_copy(M.d_t2, M.h_t2))) return rc;
     if ((rc = dev_copy(M.d_bfilt, M.h_bfilt))) return rc;
     if ((rc = dev_copy(M.d_bfilt_lds, M.h_bfilt_lds))) return rc;
-    if ((rc = dev_copy(M.d_bkey, M.h_bkey))) return rc;
+    if ((rc = dev_directory(M.d_bkey, M.h_bkey_rows, M.h_bkey_slot, M.bhcap, 64, 0u))) return rc;
     if ((rc = dev_copy(M.d_bdkey, M.h_bdkey))) return rc;
     if ((rc = dev_copy(M.d_bpf, M.h_bpf))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
@@ -2250,11 +2288,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     M.rtc_block = pf ? (M.bs_pf_log2 >= 20 ? 1024 : 512) : env_i("CVD_K1B_BLOCK", M.rtc_ldsf ? (M.fcap > ((int64_t)1 << 14) ? 1024 : 512) : kBlock);
     if (M.rtc_block != 256 && M.rtc_block != 512 && M.rtc_block != 1024) M.rtc_block = kBlock;
     const int patbits = M.rtc_ldsf ? kFilterPatBitsLds : bs ? M.bs_pat_bits : kFilterPatBits;
-    const std::string vdefs = "-DCVD_K1B_BLOCK=" + std::to_string(M.rtc_block) +
-                              (M.rtc_ldsf ? " -DCVD_K1B_LDSF=1" : "") +
-                              (patbits != kFilterPatBits ? " -DCVD_FILTER_PAT_BITS=" + std::to_string(patbits) : "") +
-                              (bs ? " -DCVD_K1B_BITSLICE=1" : "") + (pf ? " -DCVD_K1S_PF=1" : "") +
-                              (pf && M.bs_pf_log2 != kBsPfLog2Bits ? " -DCVD_K1S_PF_LOG2=" + std::to_string(M.bs_pf_log2) : "");
+    const std::string vdefs = rtc_variant_defs(M.rtc_block, M.rtc_ldsf, patbits, bs, pf, M.bs_pf_log2);
     if (rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn, &M.rtc_fn_multi) == 0) {
       M.rtc_bs = bs;
       M.rtc_pf = pf;

@@ -24,6 +24,7 @@
 // tuning defines, so a later process with the same decoder skips the compile.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <spawn.h>
 #include <sys/file.h>
@@ -71,6 +72,19 @@ std::string cache_dir() {
   return d;
 }
 
+// The prebuilt cache: code objects compiled at build time (cvd_jit_prebuild, run by
+// __graft_entry__.build() for the configured codes) in <directory of libcvd.so>/jit, looked up
+// before the user cache with the same key; read only (CVD_JIT_PREBUILT=off skips it).
+std::string prebuilt_dir() {
+  const char* e = std::getenv("CVD_JIT_PREBUILT");
+  if (e && std::string(e) == "off") return "";
+  Dl_info info;
+  if (::dladdr(reinterpret_cast<void*>(&prebuilt_dir), &info) == 0 || !info.dli_fname) return "";
+  std::string p = info.dli_fname;
+  const size_t slash = p.rfind('/');
+  return slash == std::string::npos ? "" : p.substr(0, slash) + "/jit";
+}
+
 bool cache_load(const std::string& path, std::vector<char>& code) {
   std::ifstream f(path, std::ios::binary);
   if (!f) return false;
@@ -111,6 +125,16 @@ std::string entry_source(int m, uint64_t xm) {
 bool file_exists(const std::string& p) {
   struct stat st;
   return ::stat(p.c_str(), &st) == 0;
+}
+
+std::string find_clang();
+// the cache file name of a code object: a hash of everything the compile depends on
+std::string object_name(const std::string& src, const std::string& arch, const std::string& all_defs) {
+  std::string keytxt = src + "\n" + arch + "\n" + find_clang() + "\n" + all_defs;
+  for (const char* f : kClangFlags) keytxt += std::string("\n") + f;
+  char name[64];
+  std::snprintf(name, sizeof(name), "/k1b_%016llx.co", (unsigned long long)fnv1a(keytxt));
+  return name;
 }
 
 std::string find_clang() {
@@ -264,17 +288,12 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
   std::string err1, err2;
   const char* via = std::getenv("CVD_JIT_VIA");   // "hiprtc" forces the fallback (tests)
   const bool force_rtc = via && std::string(via) == "hiprtc";
-  // on-disk cache of the clang-built code object
-  std::string cpath;
+  // on-disk cache of the clang-built code object (and the read-only prebuilt one)
+  std::string cpath, ppath;
   if (!force_rtc) {
-    const std::string dir = cache_dir();
-    std::string keytxt = src + "\n" + arch + "\n" + find_clang() + "\n" + all_defs;
-    for (const char* f : kClangFlags) keytxt += std::string("\n") + f;
-    if (!dir.empty()) {
-      char name[64];
-      std::snprintf(name, sizeof(name), "/k1b_%016llx.co", (unsigned long long)fnv1a(keytxt));
-      cpath = dir + name;
-    }
+    const std::string dir = cache_dir(), pdir = prebuilt_dir(), name = object_name(src, arch, all_defs);
+    if (!dir.empty()) cpath = dir + name;
+    if (!pdir.empty()) ppath = pdir + name;
   }
   auto load = [&](hipFunction_t& fn, hipFunction_t& fnm) {
     int cur = 0;
@@ -316,6 +335,10 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
       lk.fd = -1;
     }
   }
+  if (!ppath.empty() && cache_load(ppath, code)) {
+    if (load(fn, fnm)) return done();
+    code.clear();   // (a prebuilt object this device cannot load: the caches below)
+  }
   if (!cpath.empty() && cache_load(cpath, code)) {
     if (load(fn, fnm)) return done();
     ::unlink(cpath.c_str());   // unusable cached object: rebuild it
@@ -326,4 +349,20 @@ int cvd::rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_de
   if (!ok) { set_error("JIT: " + err1 + " | " + err2); return -1; }
   if (!load(fn, fnm)) { set_error("JIT: module load failed"); return -1; }
   return done();
+}
+
+int cvd::rtc_prebuild(int m, uint64_t xm, const char* variant_defs, const char* arch, const char* dir) {
+  if (!arch || !dir) { set_error("prebuild: null argument"); return -1; }
+  const std::string src = std::string(kRtcSource) + entry_source(m, xm);
+  const std::string defs = variant_defs ? variant_defs : "";
+  const std::string path = std::string(dir) + object_name(src, arch, defs);
+  std::vector<char> code;
+  if (cache_load(path, code)) return 0;
+  for (size_t i = 1; i <= std::string(dir).size(); ++i)
+    if (i == std::string(dir).size() || dir[i] == '/') (void)::mkdir(std::string(dir).substr(0, i).c_str(), 0755);
+  std::string err;
+  if (!compile_clang(src, arch, defs, code, err)) { set_error("prebuild: " + err); return -1; }
+  cache_store(path, code);
+  if (!file_exists(path)) { set_error("prebuild: cannot write " + path); return -1; }
+  return 0;
 }

@@ -299,6 +299,13 @@ int cvd_model_device_error(cvd_model* model, int32_t* flags_out);
  * left to the sequential rerun.  Diagnostic (tests, bench); not thread-safe. */
 int cvd_chunk_last(int64_t* out4);
 
+/* Compile the code-specialised detector's default variants for decoder `dec` and GPU
+ * architecture `arch` (e.g. "gfx950") into `dir` without a device: the prebuilt cache that
+ * model upload reads before compiling (its default: <directory of libcvd.so>/jit;
+ * CVD_JIT_PREBUILT=off skips it).  Only the bit-sliced codes (m = 6, k = 1, n = 2 standard
+ * butterflies) have variants to build; *n_built = how many were built or found. */
+int cvd_jit_prebuild(const cvd_code* dec, const char* arch, const char* dir, int32_t* n_built);
+
 /* The same grid point in ONE kernel per launch, without streams in HBM: every lane
  * generates its own sequence's received words (cvd_generate's encoder and noise, bit
  * for bit) and runs the LDS-resident table automaton on them (dense models with

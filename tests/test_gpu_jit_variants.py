@@ -71,3 +71,30 @@ def test_directory_layouts_bit_identical(pkg, dev, p, monkeypatch):
     cm = C.Model(c1, p, None, 200, 1.0, SEED)
     _, s_cpu = cm.run_trials(c1, c2, N, p, SEED, t0, t0 + 16, sums=True)
     assert np.array_equal(ref[:16], s_cpu)
+
+
+def test_prebuilt_jit_objects_are_loaded(pkg, dev, tmp_path):
+    """__graft_entry__.build() compiles the m = 6 code's default variants into the library's
+    prebuilt cache (cvd_jit_prebuild -> <package>/lib/jit); a fresh process with an EMPTY user
+    JIT cache must load them at model upload -- the lockstep (pre-filter) and walking (LDS
+    filter) variants -- and compile nothing (the user cache stays empty)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    jit = os.path.join(root, "detecting-convolutional-codes-via-markovian-statistics_amd", "lib", "jit")
+    if not os.path.isdir(jit) or not os.listdir(jit):
+        pytest.skip("no prebuilt JIT objects (build() not run)")
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from __graft_entry__ import load_package\n"
+            "pkg = load_package(); cc = pkg.CONFIG_CODES['m6']\n"
+            "det = pkg.Detector(1, 2, 6, cc['gen1'], device=0)\n"
+            "for p in (0.01, 0.05):\n"
+            "    m = det.model(p, 1000000, 200, 1.0, 12345); s = m.jit_status()\n"
+            "    assert s[0] == 1, s\n"
+            "    print(p, m.info()['lds_filter'], pkg.KERNEL_NAMES[m.info()['explicit_kernel']])\n") % root
+    env = dict(os.environ, CVD_JIT_CACHE=str(tmp_path))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bit-sliced" in out.stdout and " 1 " in out.stdout, out.stdout
+    assert not [f for f in os.listdir(tmp_path) if f.endswith(".co")], os.listdir(tmp_path)

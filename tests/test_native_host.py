@@ -229,3 +229,22 @@ def test_multi_groups_follow_variant_and_persistence(pkg, monkeypatch):
     assert g(cap) == [[0, 1, 2, 3]]          # no batch sizes: variant only
     monkeypatch.setenv("CVD_NO_MULTI", "1")
     assert g(ms[:2]) == [[0], [1]]
+
+
+def test_jit_prebuild_only_for_bit_sliced_codes(pkg):
+    """cvd_jit_prebuild compiles nothing for a code without the bit-sliced kernel (m = 2) and
+    reports the m = 6 code's variants when build() has put them in the prebuilt cache"""
+    import ctypes
+    import os
+    lib = pkg.lib()
+    cc = pkg.CONFIG_CODES["m2"]
+    n = ctypes.c_int32(-1)
+    assert lib.cvd_jit_prebuild(pkg.Code(cc["gen1"], cc["m"], cc["k"], cc["n"]).c, b"gfx950", b"/nonexistent/x",
+                                ctypes.byref(n)) == 0
+    assert n.value == 0
+    jit = os.path.join(os.path.dirname(pkg.__file__), "lib", "jit")
+    if os.path.isdir(jit) and len(os.listdir(jit)) >= 3:
+        c6 = pkg.CONFIG_CODES["m6"]
+        n6 = ctypes.c_int32(-1)
+        assert lib.cvd_jit_prebuild(pkg.Code(c6["gen1"], 6, 1, 2).c, b"gfx950", jit.encode(), ctypes.byref(n6)) == 0
+        assert n6.value == 3   # (found, not recompiled: each is already there)
