@@ -269,9 +269,11 @@ def main():
     rc = launch_ranks(a)
     if rc is not None:
         sys.exit(rc)
-    # (before any GPU call: rocm-smi in child processes)
-    box = box_identity() if int(os.environ.get("RANK", "0")) == 0 and os.environ.get("CVD_BENCH_SMI", "1") != "0" \
-        else None
+    # (before any GPU call: rocm-smi in child processes; not under a profiler, whose preloaded
+    # library would initialise the GPU in those children before their interpreter's exec)
+    profiled = any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", "")
+    box = box_identity() if (int(os.environ.get("RANK", "0")) == 0 and os.environ.get("CVD_BENCH_SMI", "1") != "0"
+                             and not profiled) else None
     import numpy as np
     import torch
     from __graft_entry__ import load_package

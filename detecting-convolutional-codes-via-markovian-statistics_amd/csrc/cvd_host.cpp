@@ -622,7 +622,10 @@ void build_hash(cvd_model& Mo) {
   while (bcap < ((int64_t)1 << bload) * Mo.n_rows) bcap <<= 1;
   // the kernel addresses the directory, the two-step records and the images by 32-bit byte
   // offsets: past 4 GiB (over ~2·10^6 rows) the model keeps the nibble tables
-  if (bcap * 256 > ((int64_t)1 << 32) || Mo.n_rows * 512 > ((int64_t)1 << 32)) Mo.bs = false;
+  // directory slots of 256 B, or three 128-B lines {two phase images, record} (CVD_BS_SLOT3=1)
+  const char* s3 = std::getenv("CVD_BS_SLOT3");
+  Mo.bs_slot_w = s3 && s3[0] == '1' ? 96 : 64;
+  if (bcap * 4 * Mo.bs_slot_w > ((int64_t)1 << 32) || Mo.n_rows * 512 > ((int64_t)1 << 32)) Mo.bs = false;
   Mo.h_bfilt.clear(); Mo.h_bfilt_lds.clear(); Mo.h_bkey_rows.clear(); Mo.h_bkey_slot.clear(); Mo.h_bdkey.clear();
   Mo.h_bpf.clear();
   Mo.bhcap = 0; Mo.bmax_probe = 0;
@@ -641,7 +644,8 @@ void build_hash(cvd_model& Mo) {
     }
     const unsigned bnpat = 1u << Mo.bs_pat_bits;
     Mo.bhcap = bcap;
-    constexpr int kSlotW = 64, kRecW = 48, kImgW = 48;
+    constexpr int kRecW = 48, kImgW = 48;
+    const int kSlotW = Mo.bs_slot_w;
     Mo.h_bkey_rows.assign((size_t)Mo.n_rows * kSlotW, 0u);   // (the empty slots: zero, c = 0 in every record)
     Mo.h_bkey_slot.assign((size_t)Mo.n_rows, 0u);
     Mo.h_bfilt.assign((size_t)fcap, 0u);
@@ -680,11 +684,16 @@ void build_hash(cvd_model& Mo) {
     parallel_for(Mo.n_rows, [&](int64_t i, int) {
       uint32_t* sp = Mo.h_bkey_rows.data() + (size_t)i * kSlotW;
       uint32_t* dk = Mo.h_bdkey.data() + (size_t)dev_of[(size_t)i] * kImgW;
+      const uint32_t* rec = Mo.h_drow.data() + (size_t)dev_of[(size_t)i] * Mo.h_rsw;
       for (int ph = 0; ph < 6; ++ph) {
-        bs_image(Mo.keys.data() + (size_t)i * M, ph, sp + 8 * ph);
-        std::memcpy(dk + 8 * ph, sp + 8 * ph, 8 * sizeof(uint32_t));
+        bs_image(Mo.keys.data() + (size_t)i * M, ph, dk + 8 * ph);
+        // (slot3: image of phase ph at dword 32 (ph / 2) + 8 (ph % 2) of the line ph / 2)
+        std::memcpy(sp + (kSlotW == 96 ? 32 * (ph / 2) + 8 * (ph % 2) : 8 * ph), dk + 8 * ph, 8 * sizeof(uint32_t));
       }
-      std::memcpy(sp + kRecW, Mo.h_drow.data() + (size_t)dev_of[(size_t)i] * Mo.h_rsw, sizeof(uint32_t) * 16);
+      if (kSlotW == 96)
+        for (int k = 0; k < 3; ++k) std::memcpy(sp + 32 * k + 16, rec, sizeof(uint32_t) * 16);
+      else
+        std::memcpy(sp + kRecW, rec, sizeof(uint32_t) * 16);
     });
   }
   pt.mark("  bit-sliced tables: images + records");

@@ -66,6 +66,8 @@ struct cvd_model {
   std::vector<uint32_t> h_bkey_rows;   // [n_rows][64]: slot contents -- images 8 words x 6 phases,
                                        // records 4 x 4 -- of the [bhcap][64] directory (empty: zero, c = 0)
   std::vector<uint32_t> h_bkey_slot;   // [n_rows]: the row's slot (< bhcap)
+  int32_t bs_slot_w = 64;         // dwords per directory slot: 64, or 96 (CVD_BS_SLOT3: three lines
+                                  // of {two phase images, the record}; kernel -DCVD_K1S_SLOT3=1)
   std::vector<uint32_t> h_bdkey;  // [n_rows][48]
   // LDS pre-filter of k1s (CVD_K1S_PF): one bit per row at bit pl >> (32 - kBsPfLog2Bits) of
   // its digest hash, 2^kBsPfLog2Bits bits (128 KiB) that a 1,024-thread block keeps in LDS;
@@ -173,7 +175,7 @@ int rtc_k1b_function(int device, int m, uint64_t xm, const char* variant_defs, v
                      void** fn_multi_out = nullptr);
 // the -D set of a specialised-kernel variant (upload_model, and cvd_jit_prebuild: the same text
 // keys the same code object)
-std::string rtc_variant_defs(int block, bool ldsf, int patbits, bool bs, bool pf, int pf_log2);
+std::string rtc_variant_defs(int block, bool ldsf, int patbits, bool bs, bool pf, int pf_log2, bool slot3 = false);
 // compile one variant for `arch` into `dir` (the prebuilt cache rtc_k1b_function reads first);
 // 0 = ok (or already there)
 int rtc_prebuild(int m, uint64_t xm, const char* variant_defs, const char* arch, const char* dir);

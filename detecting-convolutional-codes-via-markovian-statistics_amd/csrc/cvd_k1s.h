@@ -25,6 +25,21 @@ namespace cvd_dev {
 
 constexpr int kBsSlotShift = 6;      // directory slot: 64 dwords
 constexpr int kBsRecWord = 48;       // record r at dwords 48 + 4 r of a slot (images 8 x 6 before it)
+// Directory slots of three 128-B lines (CVD_K1S_SLOT3, the model's bs_slot_w = 96; cvd_host.cpp
+// build_hash): line k = {image of phase 2k, image of phase 2k + 1, the row's record}, so that a
+// candidate's image and record share one line (the 256-B slot: 2 lines for phases 0-3)
+#ifndef CVD_K1S_SLOT3
+#define CVD_K1S_SLOT3 0
+#endif
+constexpr bool kSlot3 = CVD_K1S_SLOT3 != 0;
+template <int PH>
+__device__ __forceinline__ constexpr uint32_t bs_img_off() {
+  return kSlot3 ? 128u * (PH / 2) + 32u * (PH % 2) : 32u * PH;
+}
+template <int PH>
+__device__ __forceinline__ constexpr uint32_t bs_rec_off() {
+  return kSlot3 ? 128u * (PH / 2) + 64u : 4u * kBsRecWord;
+}
 constexpr int kBsDkeyWords = 48;     // six images per row in a.dkey
 constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 // timing ablation (CVD_JIT_DEFINES=-DCVD_K1S_ABL=1; results differ): the waves of H2
@@ -171,7 +186,7 @@ struct BsCursor {
 #pragma unroll
     for (int w = 0; w < 8; ++w) asm volatile("" : "+v"(pkey[w]) : "v"(dep));
   }
-  __device__ static uint32_t slot_off(uint32_t s) { return s << (kBsSlotShift + 2); }
+  __device__ static uint32_t slot_off(uint32_t s) { return kSlot3 ? s * 384u : s << (kBsSlotShift + 2); }
   __device__ static void load_image(const uint32_t* base, uint32_t o, uint32_t (&k)[8]) {
     const uint4 u = ld_off<uint4>(base, o), v = ld_off<uint4>(base, o + 16u);
     k[0] = u.x; k[1] = u.y; k[2] = u.z; k[3] = u.w; k[4] = v.x; k[5] = v.y; k[6] = v.z; k[7] = v.w;
@@ -183,8 +198,8 @@ struct BsCursor {
     cand = slot == -2 && cvd::bs_bop3<cvd::kTtAndNotOr>(fb1, fw1, cvd::bs_bop3<cvd::kTtAndNotOr>(fb, fw, 0u)) == 0u;
     if (cand) {
       const uint32_t so = slot_off(hs);
-      load_image(a.hkey, so + 32u * PH, pkey);
-      const uint4 v = ld_off<uint4>(a.hkey, so + 4u * kBsRecWord + word_off16(r));
+      load_image(a.hkey, so + bs_img_off<PH>(), pkey);
+      const uint4 v = ld_off<uint4>(a.hkey, so + bs_rec_off<PH>() + word_off16(r));
       pc = v.w;
       pnx = (int32_t)v.z;
       plp = __hiloint2double((int)v.y, (int)v.x);
@@ -220,10 +235,10 @@ struct BsCursor {
         for (int pr = 1; pr <= a.max_probe; ++pr) {
           sl = (sl + 1u) & a.hmask;
           const uint32_t so = slot_off(sl);
-          const uint4 v = ld_off<uint4>(a.hkey, so + 4u * kBsRecWord + word_off16(r));
+          const uint4 v = ld_off<uint4>(a.hkey, so + bs_rec_off<PH>() + word_off16(r));
           if (v.w == 0u) break;
           uint32_t k[8];
-          load_image(a.hkey, so + 32u * PH, k);
+          load_image(a.hkey, so + bs_img_off<PH>(), k);
           if (same(k, R)) {
             lpv = __hiloint2double((int)v.y, (int)v.x);
             ns = (int32_t)v.z;

@@ -2220,11 +2220,12 @@ static int ck_finish(std::vector<CkGroup>& gs, hipStream_t st) {
   return rc;
 }
 
-std::string cvd::rtc_variant_defs(int block, bool ldsf, int patbits, bool bs, bool pf, int pf_log2) {
+std::string cvd::rtc_variant_defs(int block, bool ldsf, int patbits, bool bs, bool pf, int pf_log2, bool slot3) {
   return "-DCVD_K1B_BLOCK=" + std::to_string(block) + (ldsf ? " -DCVD_K1B_LDSF=1" : "") +
          (patbits != kFilterPatBits ? " -DCVD_FILTER_PAT_BITS=" + std::to_string(patbits) : "") +
          (bs ? " -DCVD_K1B_BITSLICE=1" : "") + (pf ? " -DCVD_K1S_PF=1" : "") +
-         (pf && pf_log2 != kBsPfLog2Bits ? " -DCVD_K1S_PF_LOG2=" + std::to_string(pf_log2) : "");
+         (pf && pf_log2 != kBsPfLog2Bits ? " -DCVD_K1S_PF_LOG2=" + std::to_string(pf_log2) : "") +
+         (bs && slot3 ? " -DCVD_K1S_SLOT3=1" : "");
 }
 
 int cvd::upload_model(cvd_model& M, int device) {
@@ -2254,7 +2255,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_t2, M.h_t2))) return rc;
     if ((rc = dev_copy(M.d_bfilt, M.h_bfilt))) return rc;
     if ((rc = dev_copy(M.d_bfilt_lds, M.h_bfilt_lds))) return rc;
-    if ((rc = dev_directory(M.d_bkey, M.h_bkey_rows, M.h_bkey_slot, M.bhcap, 64, 0u))) return rc;
+    if ((rc = dev_directory(M.d_bkey, M.h_bkey_rows, M.h_bkey_slot, M.bhcap, M.bs_slot_w, 0u))) return rc;
     if ((rc = dev_copy(M.d_bdkey, M.h_bdkey))) return rc;
     if ((rc = dev_copy(M.d_bpf, M.h_bpf))) return rc;
     if ((rc = dev_copy(M.d_bmp, M.bmp))) return rc;
@@ -2288,7 +2289,7 @@ int cvd::upload_model(cvd_model& M, int device) {
     M.rtc_block = pf ? (M.bs_pf_log2 >= 20 ? 1024 : 512) : env_i("CVD_K1B_BLOCK", M.rtc_ldsf ? (M.fcap > ((int64_t)1 << 14) ? 1024 : 512) : kBlock);
     if (M.rtc_block != 256 && M.rtc_block != 512 && M.rtc_block != 1024) M.rtc_block = kBlock;
     const int patbits = M.rtc_ldsf ? kFilterPatBitsLds : bs ? M.bs_pat_bits : kFilterPatBits;
-    const std::string vdefs = rtc_variant_defs(M.rtc_block, M.rtc_ldsf, patbits, bs, pf, M.bs_pf_log2);
+    const std::string vdefs = rtc_variant_defs(M.rtc_block, M.rtc_ldsf, patbits, bs, pf, M.bs_pf_log2, M.bs_slot_w == 96);
     if (rtc_k1b_function(device, M.dec.m, M.bfly_x, vdefs.c_str(), &M.rtc_fn, &M.rtc_fn_multi) == 0) {
       M.rtc_bs = bs;
       M.rtc_pf = pf;

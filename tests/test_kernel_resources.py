@@ -24,6 +24,9 @@ VARIANTS = {
     "k1s_pf": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1S_PF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10"],
     "k1s_ldsf": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1B_LDSF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10"],
     "k1s_global": ["-DCVD_K1B_BITSLICE=1"],
+    # three-line directory slots (CVD_BS_SLOT3=1, measured and not the default: profiles/r06j)
+    "k1s_pf_slot3": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1S_PF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10",
+                     "-DCVD_K1S_SLOT3=1"],
 }
 
 
