@@ -180,6 +180,7 @@ struct ExpArgs {
   // chunked detection (k1s, counts via ck_combine_kernel): unit u runs time chunk
   // u % ck_n of the 64 sequences of wave u / ck_n -- steps [j ck_len, (j + 1) ck_len), started
   // ck_warm steps early from D = 0 -- and writes its record to ck_out instead of sums / counts
+  int32_t mix;              // k1s lockstep: units alternate H1 and H2 waves (walk mode always does)
   int32_t ck_n;             // chunks per sequence (0: off)
   int32_t ck_len, ck_warm;  // steps per chunk and warm-up steps (multiples of 192)
   uint32_t* ck_out;         // [ck_n][nseq][kCkRecWords]: D at the chunk start and end (phase 0), lp, lr

@@ -533,8 +533,10 @@ __device__ __forceinline__ void ck_store(const ExpArgs& a, int64_t qwave, int32_
 template <uint64_t XM, bool kCk = false>
 __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const double* s_lt, int32_t ck_j = 0) {
   constexpr bool kUni = xm_uni<6, XM>();
-  if (a.walk) {
-    // H1 and H2 waves alternate on every SIMD (k1b_body)
+  if (a.walk || (a.mix && !kCk)) {
+    // H1 and H2 waves alternate on every SIMD (k1b_body; lockstep too where a.mix: the units of
+    // a persistent launch are taken in order, so that without it the first half of the launch
+    // runs H1 waves only and the second H2 waves only)
     const int64_t half = ((a.nseq + 63) / 64 + 1) / 2, k = gw >> 1;
     if (gw < 2 * half) gw = ((gw ^ (gw >> 2)) & 1) ? half + k : k;
   }
@@ -705,7 +707,7 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
   // units: waves of 64 sequences; walk mode's H1 / H2 interleave (k1s_wave) permutes
   // [0, 2 ceil(units / 2)), whose last unit may hold no sequence
   uint32_t nunits = (uint32_t)((a.nseq + 63) / 64);   // < 2^32 (host: grid and queue limits)
-  if (a.walk) nunits = (nunits + 1u) & ~1u;
+  if (a.walk || (a.mix && a.ck_n <= 0)) nunits = (nunits + 1u) & ~1u;
   // chunked: ck_n units (time chunks) per wave of sequences (no walk mode)
   const uint32_t ckn = a.ck_n > 0 ? (uint32_t)a.ck_n : 1u;
   nunits *= ckn;

@@ -1961,6 +1961,15 @@ static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int6
   a.pf = bs && M.rtc_pf ? M.d_bpf : nullptr;
   a.wq = nullptr;   // (launch_detect_explicit sets it for a persistent launch)
   a.ck_n = 0; a.ck_len = 0; a.ck_warm = 0; a.ck_out = nullptr;   // (ck_submit sets them for a chunked launch)
+  // Lockstep k1s units alternate H1 and H2 waves where the H1 sequences mostly walk learned rows
+  // (rows < learn_len / 2: p <= 0.05 of the sweep), so that every SIMD holds waves of both
+  // kinds: H1 waves there wait on cold directory and record lines, H2 waves mostly on the
+  // L2-resident filter.  Measured (profiles/r06k, -DCVD_K1S_MIX=1 on every p): p = 0.05 1,983 ->
+  // 1,896 ms, p = 0.1 / 0.15 +1% (their H1 and H2 waves look alike).  CVD_K1S_MIX=0 / 1 forces.
+  {
+    const int e = env_i("CVD_K1S_MIX", -1);
+    a.mix = e >= 0 ? (e != 0) : (M.kind == 1 && M.learn_len_eff > 0 && 2 * M.n_rows < M.learn_len_eff);
+  }
   a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the

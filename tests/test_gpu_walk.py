@@ -199,6 +199,26 @@ def test_persistent_launch_equals_block_launch(pkg, monkeypatch, p, walk):
     assert model.device_error() == 0
 
 
+@pytest.mark.parametrize("p", [0.05, 0.2])
+def test_mixed_unit_order_equals_in_order(pkg, monkeypatch, p):
+    """Lockstep units alternating H1 and H2 waves (ExpArgs.mix, CVD_K1S_MIX; the default where
+    rows < learn_len / 2) give the in-order launch's sums and counts, persistent and block
+    launches, a partial last unit and an odd number of units."""
+    cc, det = _m6(pkg)
+    model = det.model(p, 200_000, 200, 1.0, SEED)
+    monkeypatch.setenv("CVD_WALK", "0")
+    for N, t0, t1, blocks in [(1237, 0, 1500, "2"), (2000, 77, 77 + 2111, "0")]:
+        monkeypatch.setenv("CVD_K1S_MIX", "0")
+        monkeypatch.setenv("CVD_K1S_PERSIST_BLOCKS", blocks)
+        ref, rc = _sums(det, model, cc, N, p, t0, t1)
+        monkeypatch.setenv("CVD_K1S_MIX", "1")
+        got, gc = _sums(det, model, cc, N, p, t0, t1)
+        assert not np.isnan(got).any()
+        assert np.array_equal(got, ref), (p, N)
+        assert gc == rc
+    assert model.device_error() == 0
+
+
 @pytest.mark.parametrize("p,walk", [(0.01, "1"), (0.1, "0")])
 def test_persistent_launch_early_decision_counts(pkg, monkeypatch, p, walk):
     """Counts-only early decision under the work-queue launch (a wave that has decided its
