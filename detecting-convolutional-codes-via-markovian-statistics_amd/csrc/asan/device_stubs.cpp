@@ -27,7 +27,7 @@ int cvd::device_learn_dense(const CodeDesc&, const std::vector<int32_t>&, int64_
   cvd::set_error("no device in the host sanitizer build");
   return CVD_E_UNSUPPORTED;
 }
-std::string cvd::rtc_variant_defs(int, bool, int, bool, bool, int) { return ""; }
+std::string cvd::rtc_variant_defs(int, bool, int, bool, bool, int, bool) { return ""; }
 int cvd::rtc_prebuild(int, uint64_t, const char*, const char*, const char*) {
   cvd::set_error("no JIT in the host sanitizer build");
   return -1;
