@@ -438,6 +438,20 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
           // planes the row's image at the wave's phase; that step takes log P̂1 from
           // cur.plp with successor -1
           auto leave = [&]() {
+            // (timing ablation, CVD_WALK_ABL & 8: a lane that leaves its rows skips that step and
+            // walks on from row 0 -- the walk's own cost without the leavers' ACS steps; every
+            // leave still advances the lane, so the loop ends)
+            if (CVD_WALK_ABL & 8) {
+              cur.slot = a.slot0;
+              advance();
+              if (finished()) {
+                mode = kWalkDone;
+                cur.slot = -1;
+              } else {
+                walk_prefetch();
+              }
+              return;
+            }
             mode = kWalkAcs;
             cur.pnx = -1;
             const uint32_t ko = (uint32_t)cur.slot * (4u * kBsDkeyWords) + 32u * phw;
@@ -548,6 +562,8 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     k1s_walk<XM>(a, qwave, vmask, s_lt);
     return;
   }
+  // (timing ablation, CVD_WALK_ABL & 4: a walk launch's lockstep (H2) waves do nothing)
+  if ((CVD_WALK_ABL & 4) && a.walk) return;
   double lp = 0.0, lr = 0.0;
   if (valid) {
     uint32_t R[2][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};   // D_0 = 0
