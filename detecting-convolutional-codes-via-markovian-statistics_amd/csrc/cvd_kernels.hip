@@ -2189,9 +2189,23 @@ static int ck_submit(CkGroup& g, hipStream_t st) {
   return CVD_OK;
 }
 
+// a call that fails after queueing chunked groups: their workspaces back to the pool
+static void ck_release(std::vector<CkGroup>& gs, hipStream_t st) {
+  for (CkGroup& g : gs)
+    if (g.ws) {
+      (void)hipFreeAsync(g.ws, st);
+      g.ws = nullptr;
+    }
+}
+
 // the decisions' loose ends: the sequences ck_combine_kernel could not keep, rerun sequentially
 static int ck_finish(std::vector<CkGroup>& gs, hipStream_t st) {
   if (gs.empty()) return CVD_OK;
+  struct Rel {
+    std::vector<CkGroup>& gs;
+    hipStream_t st;
+    ~Rel() { ck_release(gs, st); }   // (every return path: the workspaces back to the pool)
+  } rel{gs, st};
   std::vector<std::vector<int32_t>> rn(gs.size());
   for (size_t x = 0; x < gs.size(); ++x) {
     rn[x].resize(2 * gs[x].m.size());
@@ -2216,12 +2230,7 @@ static int ck_finish(std::vector<CkGroup>& gs, hipStream_t st) {
       HIP_CHECK(hipFreeAsync(buf, st));
     }
   }
-  for (CkGroup& g : gs)
-    if (g.ws) {
-      HIP_CHECK(hipFreeAsync(g.ws, st));
-      g.ws = nullptr;
-    }
-  // (the redo counts of the last call, for cvd_chunk_stats)
+  // (the redo counts of the last call, for cvd_chunk_last)
   int64_t tot = 0;
   for (auto& v : rn)
     for (int32_t c : v) tot += c;
@@ -2425,7 +2434,10 @@ static int detect_one(const cvd_model* model, const uint32_t* d_r, int64_t N, in
     g.m = {model}; g.r = {d_r}; g.nseq = {nseq}; g.nh1 = {n_h1}; g.counts = {d_counts}; g.P = P; g.N = N;
     cvd::ck_last = {cvd::ck_last[0] + 1, P.C, P.L, 0};
     rc = ck_submit(g, (hipStream_t)stream);
-    if (rc) return rc;
+    if (rc) {
+      ck_release(gs, (hipStream_t)stream);
+      return rc;
+    }
     return ck_finish(gs, (hipStream_t)stream);
   }
   if (path == CVD_PATH_EXPLICIT || path == CVD_PATH_EXPLICIT_GENERIC || path == CVD_PATH_EXPLICIT_ORBIT ||
@@ -2518,7 +2530,10 @@ extern "C" int cvd_detect_multi(const cvd_model* const* models, int32_t nm, cons
       g.N = N;
       if (!g.m.empty()) {
         ck.push_back(std::move(g));
-        if ((rc = ck_submit(ck.back(), (hipStream_t)stream))) return rc;
+        if ((rc = ck_submit(ck.back(), (hipStream_t)stream))) {
+          ck_release(ck, (hipStream_t)stream);
+          return rc;
+        }
         cvd::ck_last = {cvd::ck_last[0] + 1, P.C, P.L, 0};
       }
       i = j;
@@ -2530,7 +2545,10 @@ extern "C" int cvd_detect_multi(const cvd_model* const* models, int32_t nm, cons
       j = i + 1;
       rc = detect_one(models[i], d_r[i], N, nseq[i], n_h1[i], d_sums ? d_sums[i] : nullptr, d_counts[i], path, stream);
     }
-    if (rc) return rc;
+    if (rc) {
+      ck_release(ck, (hipStream_t)stream);
+      return rc;
+    }
     i = j;
   }
   return ck_finish(ck, (hipStream_t)stream);

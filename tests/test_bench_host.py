@@ -47,3 +47,28 @@ def test_sweep_all_value_is_trials_over_time():
     assert v == pytest.approx(2 * 6 * 655_360 / (4050.0 * 1e-3)) and cov == list(range(6))
     with pytest.raises(ValueError):
         b.sweep_value([], 6, 1, 1)
+
+
+def test_box_record_parsing(monkeypatch):
+    """The box record (bench.py box_identity / ClockSampler): the visible cards follow the
+    HIP visibility list, and the medians under load parse rocm-smi's clock / power strings."""
+    b = _bench()
+    d = {"card0": {}, "card1": {}, "card2": {}, "system": {}}
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2")
+    assert b._visible_cards(d) == ["card2"]
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    assert b._visible_cards(d) == ["card0", "card1", "card2"]
+    s = b.ClockSampler(period=1.0)
+    s.samples = [{"card0": {"sclk clock speed:": "(2383Mhz)", "Current Socket Graphics Package Power (W)": "1344.0",
+                            "Temperature (Sensor junction) (C)": "58.0", "Card SKU": "N/A"}},
+                 {"card0": {"sclk clock speed:": "(2100Mhz)", "Current Socket Graphics Package Power (W)": "1300.0",
+                            "Temperature (Sensor junction) (C)": "57.0"}},
+                 {"card0": {"sclk clock speed:": "(2390Mhz)", "Current Socket Graphics Package Power (W)": "1350.0",
+                            "Temperature (Sensor junction) (C)": "59.0"}}]
+    med = s.summary()["median_under_load"]["card0"]
+    assert med["sclk clock speed:"] == 2383.0
+    assert med["Current Socket Graphics Package Power (W)"] == 1344.0
+    assert med["Temperature (Sensor junction) (C)"] == 58.0
+    assert "Card SKU" not in med
