@@ -69,6 +69,9 @@ constexpr int kBsEarlyGroups = 21;   // early-decision check every 126 steps
 #define CVD_K1S_TRIM 0
 #endif
 constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
+#ifndef CVD_K1S_MIDPOS
+#define CVD_K1S_MIDPOS 0
+#endif
 // chunked launches (-DCVD_K1S_CK=0 compiles them out, for A/Bs of the unchunked
 // loop's code: the host then must not chunk, CVD_CHUNK=0)
 #ifndef CVD_K1S_CK
@@ -327,10 +330,23 @@ __device__ __forceinline__ void bs_step(const ExpArgs& a, BsCursor& cur, const u
   const uint4 E0 = et[0], E1 = et[1];
   const uint32_t e0[2] = {E0.x, E1.x}, e1[2] = {E0.y, E1.y}, ez[2] = {E0.z, E1.z};
   uint32_t mu;
-  cvd::bs_step_core<PH, kUni>(R, e0, e1, ez, N, mu, c, [&](uint32_t dep) {
-    cur.fence_mid(dep);              // dep: the first word's ACS result
+  // where the candidate test and its directory loads go (CVD_K1S_MIDPOS, timing studies): 0
+  // between the two words' ACS (default), 1 at the step's start (the directory lines get the
+  // whole ACS, the filter word only the resolve before it), 2 after the ACS
+  if constexpr (CVD_K1S_MIDPOS == 1) {
+    cur.fence_mid(R[0][3]);
     cur.template mid<PH>(a, rr);
+  }
+  cvd::bs_step_core<PH, kUni>(R, e0, e1, ez, N, mu, c, [&](uint32_t dep) {
+    if constexpr (CVD_K1S_MIDPOS == 0) {
+      cur.fence_mid(dep);            // dep: the first word's ACS result
+      cur.template mid<PH>(a, rr);
+    }
   });
+  if constexpr (CVD_K1S_MIDPOS == 2) {
+    cur.fence_mid(N[1][3]);
+    cur.template mid<PH>(a, rr);
+  }
   cur.template hash_ahead<(PH + 1) % 6>(a, N);   // D_t's filter read before D_{t-1}'s loads are waited for
   cur.fence_resolve(N[1][3]);        // N[1][3] depends on the whole ACS
 }
