@@ -677,10 +677,13 @@ def main():
     latency_bound = (not parity and not lds_diag and info.get("kind") == 1 and info.get("explicit_kernel") == 5)
     bound_basis = None
     if latency_bound:
-        bound_basis = ("dependent row lookups (L2 / Infinity Cache latency) at 4 waves per SIMD: -5% modelled VALU "
-                       "issue -> <= 1% measured at p >= 0.05 (profiles/r05aq); scheduler strategies within 0.1% "
-                       "(profiles/r05ae); H2 filter reads skipped (timing only) -> p = 0.2 -9% (profiles/r05w); waves "
-                       "wait on memory 46-50% of their cycles (SQ_WAIT_ANY, valu.wave_cycles_split)")
+        bound_basis = ("dependent row lookups (the L2 filter word of every lookup, cold directory lines of re-entries) "
+                       "at 4 waves per SIMD, together with VALU issue (counted VALU 0.47-0.50 of the 2-cycle peak): not "
+                       "HBM (0.009 of peak) and not lookup bytes (three-line slots: FETCH -18-25%, time +1%, "
+                       "profiles/r06j); -5% modelled VALU issue -> <= 1% at p >= 0.05 (profiles/r05aq); scheduler "
+                       "strategies within 0.1% (profiles/r05ae); less time for the filter word -1.7% (profiles/r06o); "
+                       "H1/H2 waves mixed per SIMD -4.4% at p = 0.05 (profiles/r06k); H2 filter reads skipped (timing "
+                       "only) p = 0.2 -9% (profiles/r05w); waves wait on memory 46-53% of their cycles (SQ_WAIT_ANY)")
     elif lds_diag:
         bound_basis = "LDS array busy (roofline.lds, profiles/pmc_lds_<config>.json)"
     c = counts.cpu().numpy()
