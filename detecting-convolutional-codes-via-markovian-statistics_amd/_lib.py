@@ -42,7 +42,7 @@ class cvd_model_info(ctypes.Structure):
                 ("max_probe", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("logp1_unseen", ctypes.c_double), ("explicit_kernel", ctypes.c_int32),
                 ("mc_fused", ctypes.c_int32), ("walk", ctypes.c_int32), ("lds_filter", ctypes.c_int32),
-                ("pad0", ctypes.c_int32), ("multi_variant", ctypes.c_int64), ("persist_seqs", ctypes.c_int64)]
+                ("walk_compact", ctypes.c_int32), ("multi_variant", ctypes.c_int64), ("persist_seqs", ctypes.c_int64)]
 
 
 KERNEL_NAMES = {0: "none", 1: "detect_explicit_kernel (generic explicit path)",

@@ -181,6 +181,10 @@ struct ExpArgs {
   // u % ck_n of the 64 sequences of wave u / ck_n -- steps [j ck_len, (j + 1) ck_len), started
   // ck_warm steps early from D = 0 -- and writes its record to ck_out instead of sums / counts
   int32_t mix;              // k1s lockstep: units alternate H1 and H2 waves (walk mode always does)
+  int32_t t2c;              // k1s walk with the LDS filter: t2 holds the compact 8-B two-step records
+  int32_t nvtab;            // (t2c) values in the log P̂1 table, copied into dynamic LDS at vtab_off
+  uint32_t vtab_off;
+  const double* vtab;
   int32_t ck_n;             // chunks per sequence (0: off)
   int32_t ck_len, ck_warm;  // steps per chunk and warm-up steps (multiples of 192)
   uint32_t* ck_out;         // [ck_n][nseq][kCkRecWords]: D at the chunk start and end (phase 0), lp, lr

@@ -701,6 +701,8 @@ void build_hash(cvd_model& Mo) {
   // (r1, r2), 32 B {log P̂1(d, r1), log P̂1(d1, r2), (d1 + 1) | c(d, r1) << 28,
   // (d2 + 1) | c(d1, r2) << 28}, d1 / d2 the rows after one / two steps (0 = not a row)
   Mo.h_t2.clear();
+  Mo.h_t2c.clear();
+  Mo.h_vtab.clear();
   // (CVD_BS_T2=1: for the bit-sliced lockstep lanes too, whose kernel reads them with
   // -DCVD_K1S_T2=1 in CVD_JIT_DEFINES; timing studies, cvd_k1s.h)
   const char* bt2 = std::getenv("CVD_BS_T2");
@@ -724,6 +726,37 @@ void build_hash(cvd_model& Mo) {
         }
       }
     });
+    // the compact form (CVD_WALK_T2C=1; 8 B per record for the k1s walk, a quarter of the
+    // table's bytes: at p = 0.01's 29,626 rows 3.8 MB instead of 15 MB) where rows + 1 fit 16
+    // bits and the distinct log P̂1 values 12.  Same sums; p = 0.01 1,498 against 1,500-1,505 ms
+    // per launch (profiles/r06p): the walk waits on its dependent chain, not on the table's
+    // size, so it is not the default
+    const char* t2c = std::getenv("CVD_WALK_T2C");
+    if (Mo.bs && Mo.n_rows < 65535 && t2c && t2c[0] == '1') {
+      std::vector<uint64_t> bits(Mo.logp1.size());
+      std::memcpy(bits.data(), Mo.logp1.data(), bits.size() * sizeof(double));
+      std::sort(bits.begin(), bits.end());
+      bits.erase(std::unique(bits.begin(), bits.end()), bits.end());
+      if (bits.size() <= 4096) {
+        Mo.h_vtab.resize(bits.size());
+        std::memcpy(Mo.h_vtab.data(), bits.data(), bits.size() * sizeof(double));
+        auto idx = [&](uint32_t lo, uint32_t hi) -> uint64_t {
+          const uint64_t b = (uint64_t)lo | ((uint64_t)hi << 32);
+          return (uint64_t)(std::lower_bound(bits.begin(), bits.end(), b) - bits.begin());
+        };
+        Mo.h_t2c.assign((size_t)Mo.n_rows * 16 * 2, 0u);
+        parallel_for(Mo.n_rows, [&](int64_t d, int) {
+          for (int q = 0; q < 16; ++q) {
+            const uint32_t* e = Mo.h_t2.data() + ((size_t)d * 16 + (size_t)q) * 8;
+            const uint64_t d1 = e[4] & 0x0FFFFFFFu, c1 = e[4] >> 28, d2 = e[5] & 0x0FFFFFFFu, c2 = e[5] >> 28;
+            const uint64_t i1 = idx(e[0], e[1]), i2 = d1 ? idx(e[2], e[3]) : 0u;
+            const uint64_t w = i1 | (i2 << 12) | (d1 << 24) | (c1 << 40) | (d2 << 43) | (c2 << 59);
+            Mo.h_t2c[((size_t)d * 16 + (size_t)q) * 2] = (uint32_t)w;
+            Mo.h_t2c[((size_t)d * 16 + (size_t)q) * 2 + 1] = (uint32_t)(w >> 32);
+          }
+        });
+      }
+    }
   }
 }
 
@@ -1261,7 +1294,7 @@ extern "C" int cvd_model_info_get(const cvd_model* Mo, cvd_model_info* info) {
   info->walk = Mo->k1b_ok && Mo->hcap > 0 && walk_preferred(*Mo) && (Mo->device < 0 || Mo->rtc_fn) ? 1 : 0;
   info->lds_filter = Mo->device >= 0 ? (Mo->rtc_fn && Mo->rtc_ldsf ? 1 : 0)
                                      : (Mo->k1b_ok && Mo->hcap > 0 && ldsf_preferred(*Mo) ? 1 : 0);
-  info->pad0 = 0;
+  info->walk_compact = Mo->device >= 0 && Mo->rtc_t2c ? 1 : 0;
   info->multi_variant = multi_variant(*Mo);
   info->persist_seqs = persist_seqs(*Mo);
   return CVD_OK;

@@ -54,6 +54,11 @@ struct cvd_model {
                                   // dword 3 of entry r = the T_ref count c(r)
   std::vector<uint32_t> h_dkey;   // [n_rows][NW]: row keys (device layout) by device row id
   std::vector<uint32_t> h_t2;     // [n_rows][16][8]: two-step walk records (walking models only)
+  // the same records in 8 B (k1s walk with the LDS filter, where they fit: rows < 2^16 and at
+  // most 4,096 distinct log P̂1): bits 0-11 / 12-23 the two steps' log P̂1 as indices into
+  // h_vtab, 24-39 / 43-58 row after one / two steps + 1, 40-42 / 59-61 their T_ref counts
+  std::vector<uint32_t> h_t2c;    // [n_rows][16][2]
+  std::vector<double> h_vtab;     // the distinct log P̂1 values (exact doubles)
   // bit-sliced tables of the m = 6 kernel k1s (cvd_bitslice.h, cvd_k1s.h), beside the nibble
   // ones (which the other kernels and the trace path read): the Bloom filter over the
   // canonical digest hash, the directory of 256-B slots {six phase images, record}, and six
@@ -109,6 +114,9 @@ struct cvd_model {
   uint32_t* d_drow = nullptr;
   uint32_t* d_dkey = nullptr;
   uint32_t* d_t2 = nullptr;
+  uint32_t* d_t2c = nullptr;
+  double* d_vtab = nullptr;
+  bool rtc_t2c = false;           // the k1s walk reads d_t2c with the value table in LDS
   uint32_t* d_bfilt = nullptr;
   uint32_t* d_bfilt_lds = nullptr;
   uint32_t* d_bkey = nullptr;

@@ -173,7 +173,7 @@ struct BsCursor {
   __device__ void start(const ExpArgs& a, uint32_t r0, uint32_t r1) {
     slot = a.slot0; hs = 0u; hsn = 0u; fb = 0u; fw = 0u; fb1 = 0u; fw1 = 0u; cand = false; pc = 1u; half = 0u;
     plp2 = 0.0; pnx2 = -1;
-    if (kK1sT2 && a.t2) prefetch_t2(a, slot, r0, r1);
+    if (kK1sT2 && a.t2 && !a.t2c) prefetch_t2(a, slot, r0, r1);
     else prefetch_row(a, slot, r0);
   }
   // ordering fences (RowCursor::fence): the waits for the loads issued a step / half a step
@@ -312,7 +312,7 @@ struct BsCursor {
   template <bool kRow = true>
   __device__ void next(const ExpArgs& a, uint32_t rn, uint32_t rnn = 0u) {
     if (kRow && slot >= 0 && (!kK1sT2 || half != 2u)) {
-      if (kK1sT2 && a.t2) prefetch_t2(a, slot, rn, rnn);
+      if (kK1sT2 && a.t2 && !a.t2c) prefetch_t2(a, slot, rn, rnn);
       else prefetch_row(a, slot, rn);
     }
     hs = hsn;
@@ -385,7 +385,18 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   auto two_steps = [&]() -> bool { return a.t2 != nullptr && pos + 2u <= N; };
   auto walk_prefetch = [&]() {
     const uint32_t x = __builtin_amdgcn_alignbit(nxtw, curw, 2u * (pos & 15u));   // r of steps pos + 1, pos + 2
-    if (two_steps()) {
+    if (two_steps() && a.t2c) {
+      // the compact record (8 B, cvd_host.cpp t2c): both steps' log P̂1 as indices into the
+      // model's value table, copied into LDS by the block; rows + 1 in 16 bits, c in 3
+      uint32_t o;
+      asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(o) : "v"(x & 15u), "v"((uint32_t)cur.slot << 7));
+      const uint2 e = ld_off<uint2>(a.t2, o);
+      const double* vt = reinterpret_cast<const double*>(reinterpret_cast<const char*>(dyn_lds()) + a.vtab_off);
+      cur.plp = vt[e.x & 0xFFFu];
+      plp2 = vt[(e.x >> 12) & 0xFFFu];
+      cur.pnx = (int32_t)(__builtin_amdgcn_alignbit(e.y, e.x, 24u) & 0xFFFFu) | (int32_t)(((e.y >> 8) & 7u) << 28);
+      cur.pc = ((e.y >> 11) & 0xFFFFu) | (((e.y >> 27) & 7u) << 28);
+    } else if (two_steps()) {
       uint32_t o;
       asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(o) : "v"(x & 15u), "v"((uint32_t)cur.slot << 9));
       const uint4 v = ld_off<uint4>(a.t2, o);
@@ -726,6 +737,10 @@ __device__ __forceinline__ void k1s_body(const ExpArgs& a, uint32_t blk) {
     uint4* d = reinterpret_cast<uint4*>(dyn_lds());
     const uint4* g = reinterpret_cast<const uint4*>(a.filt);
     for (uint32_t i = threadIdx.x; i < (a.fmask + 1u) / 2u; i += blockDim.x) d[i] = g[i];
+  }
+  if (a.t2c) {   // the compact walk records' value table, after the filter
+    double* d = reinterpret_cast<double*>(reinterpret_cast<char*>(dyn_lds()) + a.vtab_off);
+    for (int32_t i = (int32_t)threadIdx.x; i < a.nvtab; i += (int32_t)blockDim.x) d[i] = a.vtab[i];
   }
 #elif CVD_K1S_PF
   {   // the pre-filter, 2^kBsPfLog2Bits bits, into dynamic LDS

@@ -1927,7 +1927,8 @@ int64_t cvd::persist_grid(const cvd_model& M, int64_t nseq) {
 
 // dynamic LDS of the specialised kernel: the LDS-resident filter or the k1s pre-filter
 static unsigned rtc_dyn_lds(const cvd_model& M) {
-  if (M.rtc_ldsf) return (unsigned)(M.fcap * sizeof(uint32_t));
+  // (the LDS filter, then -- compact walk records -- their value table)
+  if (M.rtc_ldsf) return (unsigned)(M.fcap * sizeof(uint32_t) + (M.rtc_t2c ? M.h_vtab.size() * sizeof(double) : 0));
   if (M.rtc_pf) return (unsigned)(M.h_bpf.size() * sizeof(uint32_t));
   return 0u;
 }
@@ -1971,6 +1972,16 @@ static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int6
     a.mix = e >= 0 ? (e != 0) : (M.kind == 1 && M.learn_len_eff > 0 && 2 * M.n_rows < M.learn_len_eff);
   }
   a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
+  // the k1s walk with the LDS filter reads the compact 8-B records, their log P̂1 values from a
+  // table the block copies into LDS after the filter (rtc_t2c, upload_model)
+  a.t2c = 0; a.nvtab = 0; a.vtab_off = 0u; a.vtab = nullptr;
+  if (a.t2 && which == CVD_KERNEL_BUTTERFLY_RTC && M.rtc_bs && M.rtc_ldsf && M.rtc_t2c) {
+    a.t2 = M.d_t2c;
+    a.t2c = 1;
+    a.vtab = M.d_vtab;
+    a.nvtab = (int32_t)M.h_vtab.size();
+    a.vtab_off = (uint32_t)(M.fcap * sizeof(uint32_t));
+  }
   a.walk = which == CVD_KERNEL_BUTTERFLY_RTC && !d_trace && N < ((int64_t)1 << 31) && M.d_dkey && walk_preferred(M, a.early);
   // schedule: walk while >= 48 lanes walk (a burst costs its load latency whatever the
   // lanes), or while < 4 lanes wait for the ACS (profiles/r03i_walk/ab_policy.jsonl; with
@@ -2271,6 +2282,8 @@ int cvd::upload_model(cvd_model& M, int device) {
     if ((rc = dev_copy(M.d_drow, M.h_drow))) return rc;
     if ((rc = dev_copy(M.d_dkey, M.h_dkey))) return rc;
     if ((rc = dev_copy(M.d_t2, M.h_t2))) return rc;
+    if ((rc = dev_copy(M.d_t2c, M.h_t2c))) return rc;
+    if ((rc = dev_copy(M.d_vtab, M.h_vtab))) return rc;
     if ((rc = dev_copy(M.d_bfilt, M.h_bfilt))) return rc;
     if ((rc = dev_copy(M.d_bfilt_lds, M.h_bfilt_lds))) return rc;
     if ((rc = dev_directory(M.d_bkey, M.h_bkey_rows, M.h_bkey_slot, M.bhcap, M.bs_slot_w, 0u))) return rc;
@@ -2322,6 +2335,16 @@ int cvd::upload_model(cvd_model& M, int device) {
     M.rtc_ldsf = false;
     M.rtc_block = kBlock;
   }
+  // compact walk records: where the k1s walk variant runs with the LDS filter and the value
+  // table fits beside it and the kernel's static LDS (CVD_WALK_T2C=0 at build: not built)
+  M.rtc_t2c = false;
+  if (M.rtc_fn && M.rtc_bs && M.rtc_ldsf && M.d_t2c && M.d_vtab) {
+    int st = 0, mx = 0;
+    if (hipFuncGetAttribute(&st, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, (hipFunction_t)M.rtc_fn) == hipSuccess &&
+        hipDeviceGetAttribute(&mx, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) == hipSuccess &&
+        (int64_t)st + M.fcap * 4 + (int64_t)M.h_vtab.size() * 8 <= (int64_t)mx)
+      M.rtc_t2c = true;
+  }
   // persistent launches of k1s: as many blocks as the device keeps resident
   M.rtc_persist_grid = 0;
   if (M.rtc_fn && M.rtc_bs) {
@@ -2340,12 +2363,14 @@ void cvd::free_model_device(cvd_model& M) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(M.device);
-  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_filt_lds, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2, M.d_bmp,
+  void* ptrs[] = {M.d_rec, M.d_logp1, M.d_ltref, M.d_filt, M.d_filt_lds, M.d_hkey, M.d_hrow, M.d_drow, M.d_dkey, M.d_t2,
+                  M.d_t2c, M.d_vtab, M.d_bmp,
                   M.d_bmk1, M.d_bfly, M.d_err, M.d_bfilt, M.d_bfilt_lds, M.d_bkey, M.d_bdkey, M.d_bpf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   M.d_rec = nullptr; M.d_logp1 = nullptr; M.d_ltref = nullptr;
   M.d_filt = nullptr; M.d_filt_lds = nullptr; M.d_hkey = nullptr; M.d_hrow = nullptr; M.d_drow = nullptr; M.d_dkey = nullptr; M.d_t2 = nullptr;
+  M.d_t2c = nullptr; M.d_vtab = nullptr; M.rtc_t2c = false;
   M.d_bfilt = nullptr; M.d_bfilt_lds = nullptr; M.d_bkey = nullptr; M.d_bdkey = nullptr; M.d_bpf = nullptr;
   M.rtc_persist_grid = 0;
   M.rtc_bs = false;

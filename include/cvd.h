@@ -94,7 +94,10 @@ typedef struct cvd_model_info {
                               (walking models of <= 32,768 rows: 128 KiB in 1,024-thread blocks for the
                               bit-sliced kernel, 64 KiB in 512-thread blocks for the butterfly kernel;
                               CVD_NO_LDSF=1 keeps it in global memory) */
-  int32_t pad0;
+  int32_t walk_compact;    /* 1: the walk reads 8-B two-step records whose log P̂1 values come from a
+                              table in LDS beside the filter (built with CVD_WALK_T2C=1 where rows <
+                              2^16, <= 4,096 distinct values and room in LDS; same sums, measured
+                              neutral, off by default) */
   int64_t multi_variant;   /* nonzero: the specialised kernel variant this model runs in a
                               cvd_detect_multi launch; consecutive models with equal nonzero values
                               share one launch (at most 8), except a model whose own launch would be

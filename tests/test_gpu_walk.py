@@ -41,6 +41,34 @@ def test_walk_equals_lockstep(pkg, monkeypatch, p):
     assert model.device_error() == 0      # no walk wave left its loop by the guard
 
 
+def test_compact_walk_records_equal_full_records(pkg, monkeypatch):
+    """The walk's compact 8-B two-step records (log P̂1 as indices into a value table the block
+    keeps in LDS beside the filter; cvd_model_info.walk_compact) give the 32-B records' sums
+    and counts -- and the lockstep kernel's -- bit for bit, at the headline's p = 0.01 model
+    (10^6-step chain: 29,626 rows, 2,110 distinct values)."""
+    cc, det = _m6(pkg)
+    p = 0.01
+    monkeypatch.setenv("CVD_WALK", "1")
+    monkeypatch.setenv("CVD_WALK_T2C", "1")
+    m1 = pkg.Model(det.dec, p, 1_000_000, 200, 1.0, SEED).upload(0)
+    monkeypatch.delenv("CVD_WALK_T2C")
+    i1 = m1.info()
+    assert i1["walk_compact"] == 1 and i1["lds_filter"] == 1 and i1["walk"] == 1, i1
+    m0 = pkg.Model(det.dec, p, 1_000_000, 200, 1.0, SEED).upload(0)
+    assert m0.info()["walk_compact"] == 0
+    for N, t0, t1 in [(4093, 5, 5 + 900), (20_000, 2_000_001, 2_000_001 + 256)]:
+        got, gc = _sums(det, m1, cc, N, p, t0, t1)
+        ref, rc = _sums(det, m0, cc, N, p, t0, t1)
+        assert not np.isnan(got).any()
+        assert np.array_equal(got, ref), N
+        assert gc == rc
+        monkeypatch.setenv("CVD_WALK", "0")
+        lock, lc = _sums(det, m1, cc, N, p, t0, t1)
+        monkeypatch.setenv("CVD_WALK", "1")
+        assert np.array_equal(got, lock), N
+    assert m1.device_error() == 0 and m0.device_error() == 0
+
+
 @pytest.mark.parametrize("wmin,amin,burst", [("1", "64", "1"), ("64", "1", "3"), ("8", "16", "64")])
 def test_walk_schedules(pkg, monkeypatch, wmin, amin, burst):
     """Schedule knobs change only the order of work, never a sum."""
