@@ -97,6 +97,16 @@ __device__ __forceinline__ uint32_t word_param(uint32_t r) { return kR16 ? 16u *
 #ifndef CVD_K1S_NT_STREAM
 #define CVD_K1S_NT_STREAM 1
 #endif
+// Walk mode's stream words (k1s_walk): 0 (default) -- one 4-B load per word, at the top of the
+// loop iteration after the lane moves into its next word; 1 / 2 -- whole 16-B chunks, the next
+// chunk requested for the wave's lanes together once one of them is in word >= CVD_WALK_BUF of its
+// chunk (bursts move a lane <= 16 steps, so 1 and 2 are the values that load a chunk before it is
+// read).  Same sums; p = 0.01 1,579-1,585 (1) / 1,572-1,573 (2) against 1,499-1,505 ms (0) per
+// launch on one box (profiles/r06q): the stream words' loads are not what the walk waits on
+#ifndef CVD_WALK_BUF
+#define CVD_WALK_BUF 0
+#endif
+static_assert(CVD_WALK_BUF >= 0 && CVD_WALK_BUF <= 2, "CVD_WALK_BUF: 0, 1 or 2");
 typedef unsigned int bs_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 stream_load(const uint4* p) {
   if constexpr (CVD_K1S_NT_STREAM != 0) {
@@ -368,12 +378,44 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   };
   uint32_t pos = 0u, curw = 0u, nxtw = 0u;
   bool need = false;
-  auto word_at = [&]() -> uint32_t { return curw >> (2u * (pos & 15u)); };
+  // CVD_WALK_BUF: the lane's stream as two whole 16-B chunks, ca (holding word pos / 16) and cb
+  // (the next one), read by one non-temporal load each.  A lane that moves into cb's chunk needs
+  // the chunk after it (needb); the wave requests those chunks together, at the top of the first
+  // loop iteration where such a lane has reached its chunk's word 1 -- 32 steps before the lane
+  // can read cb -- so that one stream load holds up the waits of the record loads behind it
+  // (loads complete in issue order) every few iterations instead of every iteration
+  uint4 ca = make_uint4(0u, 0u, 0u, 0u), cb = make_uint4(0u, 0u, 0u, 0u);
+  bool needb = false;
+  auto load_chunk = [&](uint32_t ci) -> uint4 {
+    if (4u * ci >= nwords) return make_uint4(0u, 0u, 0u, 0u);
+    return stream_load(reinterpret_cast<const uint4*>(a.r + (size_t)ci * cstride + (size_t)(qwave + lane_id()) * 4));
+  };
+  // the words pos / 16 and pos / 16 + 1 (CVD_WALK_BUF: picked from the chunks at each use, so that
+  // the chunks take 6 VGPRs more than the two words instead of 8; the words of a chunk past the
+  // stream's end are never read for a step < N)
+  auto cur_word = [&]() -> uint32_t {
+    if constexpr (CVD_WALK_BUF == 0) return curw;
+    const uint32_t i = (pos >> 4) & 3u;
+    return i == 0u ? ca.x : i == 1u ? ca.y : i == 2u ? ca.z : ca.w;
+  };
+  auto nxt_word = [&]() -> uint32_t {
+    if constexpr (CVD_WALK_BUF == 0) return nxtw;
+    const uint32_t i = (pos >> 4) & 3u;
+    return i == 0u ? ca.y : i == 1u ? ca.z : i == 2u ? ca.w : cb.x;
+  };
+  auto word_at = [&]() -> uint32_t { return cur_word() >> (2u * (pos & 15u)); };
   auto advance = [&]() {
     ++pos;
     if ((pos & 15u) == 0u) {
-      curw = nxtw;
-      need = true;
+      if constexpr (CVD_WALK_BUF != 0) {
+        if (((pos >> 4) & 3u) == 0u) {
+          ca = cb;
+          needb = true;
+        }
+      } else {
+        curw = nxtw;
+        need = true;
+      }
     }
   };
   uint32_t R[2][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
@@ -384,7 +426,7 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   double plp2 = 0.0;
   auto two_steps = [&]() -> bool { return a.t2 != nullptr && pos + 2u <= N; };
   auto walk_prefetch = [&]() {
-    const uint32_t x = __builtin_amdgcn_alignbit(nxtw, curw, 2u * (pos & 15u));   // r of steps pos + 1, pos + 2
+    const uint32_t x = __builtin_amdgcn_alignbit(nxt_word(), cur_word(), 2u * (pos & 15u));   // r of steps pos + 1, pos + 2
     if (two_steps() && a.t2c) {
       // the compact record (8 B, cvd_host.cpp t2c): both steps' log P̂1 as indices into the
       // model's value table, copied into LDS by the block; rows + 1 in 16 bits, c in 3
@@ -417,8 +459,13 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
     return dec != 0;
   };
   if (valid && N > 0u) {
-    curw = load_word(0u);
-    nxtw = load_word(1u);
+    if constexpr (CVD_WALK_BUF != 0) {
+      ca = load_chunk(0u);
+      cb = load_chunk(1u);
+    } else {
+      curw = load_word(0u);
+      nxtw = load_word(1u);
+    }
     cur.slot = a.slot0;   // D_0 = 0 is a learned row: every lane starts walking
     walk_prefetch();
     mode = kWalkWalk;
@@ -451,7 +498,14 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   const uint32_t wmin = (uint32_t)a.walk_wmin, amin = (uint32_t)a.walk_amin;
   const int burst = a.walk_burst;
   for (int64_t it = 0, it_max = CVD_WALK_GUARD * ((int64_t)N + 1); it < it_max; ++it) {
-    if (need) {
+    if constexpr (CVD_WALK_BUF != 0) {
+      // (a burst moves a lane <= 16 steps, so a lane in word 0 of its chunk at one iteration's
+      // top is past word 1 at a later top before it reaches word 3, where it reads cb)
+      if (__ballot(needb && ((pos >> 4) & 3u) >= (uint32_t)CVD_WALK_BUF) != 0u && needb) {
+        cb = load_chunk((pos >> 6) + 1u);
+        needb = false;
+      }
+    } else if (need) {
       nxtw = load_word((pos >> 4) + 1u);
       need = false;
     }
