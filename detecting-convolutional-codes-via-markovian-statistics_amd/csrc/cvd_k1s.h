@@ -361,6 +361,154 @@ __device__ __forceinline__ void bs_step(const ExpArgs& a, BsCursor& cur, const u
   cur.fence_resolve(N[1][3]);        // N[1][3] depends on the whole ACS
 }
 
+// the ACS of one step alone (the deep pipeline's lookups run after it)
+template <int PH, bool kUni>
+__device__ __forceinline__ void bs_acs(const uint32_t (&R)[2][4], uint32_t rr, uint32_t (&N)[2][4], uint32_t& c) {
+  const uint4* et = kR16 ? reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(bs_etab_lds()) + PH * 128 +
+                                                          cvd::bs_shl<1>(rr))
+                        : bs_etab_lds() + (PH * 4 + rr) * 2;
+  const uint4 E0 = et[0], E1 = et[1];
+  const uint32_t e0[2] = {E0.x, E1.x}, e1[2] = {E0.y, E1.y}, ez[2] = {E0.z, E1.z};
+  uint32_t mu;
+  cvd::bs_step_core<PH, kUni>(R, e0, e1, ez, N, mu, c);
+}
+
+// Two-step lookup pipeline for the lockstep lanes (CVD_K1S_DEEP): every load of a lookup gets a
+// whole step of the wave's other work to land, instead of half of one.  At step t (after the ACS
+// that makes D_{t+1} from R = D_t):
+//   resolve_a -- D_{t-1}'s lookup (planes Rp, loaded during step t-1): log P̂1(row(D_{t-1}), r_{t-1})
+//                and D_t's state (a row from the successor record, -1 not a row, -2 pending);
+//   mid_b     -- D_t: a known row's record for r_t, or, pending, the candidate test on the filter
+//                word requested at step t-1 and on a positive the home slot's image and record;
+//   hash_ahead (BsCursor's) -- D_{t+1}'s filter word where row(D_t) is not known.
+// So lp takes each P̂1 term one step later (the same terms in the same order), and a drain after
+// the last step resolves the last lookup.  The cost: the planes of D_{t-1} stay live for a step.
+// =2: D_{t+1}'s hash, pattern and pre-filter test go before the wait, so every load has the ACS
+// and the hash (~110 VALU of the step's ~165) to land.  Same sums (the parity, walk, multi,
+// config, early, chunked and C0 suites: 119 passed); same-box launches (profiles/r06u, ms, two
+// rounds): p = 0.05 / 0.1 / 0.2 1,845-1,849 / 2,051-2,052 / 1,941-1,973 (0), 1,871-1,875 /
+// 2,079-2,080 / 2,003-2,004 (1), 1,850 / 2,043-2,044 / 1,956-1,959 (2).  More time for the
+// lookups' loads buys nothing, so their latency is not what the lockstep loop waits on; off
+#ifndef CVD_K1S_DEEP
+#define CVD_K1S_DEEP 0
+#endif
+struct BsDeep : BsCursor {
+  // (the candidate's word rides in the top bits of its home slot, for the probes: hmask < 2^28)
+  static constexpr int kWordShift = 28;
+  template <int PH>
+  __device__ double resolve_a(const ExpArgs& a, const uint32_t (&Rp)[2][4], double lpu, int32_t& ns) {
+    double lpv = lpu;
+    ns = pfpos ? -2 : -1;   // D_t's lookup pending (its filter word is in), or settled by the pre-filter
+    if (slot >= 0) {
+      lpv = plp; ns = pnx;
+    } else if (cand) {
+      if (same(pkey, Rp)) {
+        lpv = plp; ns = pnx;
+      } else if (pc != 0u) {
+        // the home slot holds another row (an empty slot has c = 0): linear probing up to an
+        // empty slot
+        const uint32_t r16 = word_param(hs >> kWordShift);
+        uint32_t sl = hs & a.hmask;
+        for (int pr = 1; pr <= a.max_probe; ++pr) {
+          sl = (sl + 1u) & a.hmask;
+          const uint32_t so = slot_off(sl);
+          const uint4 v = ld_off<uint4>(a.hkey, so + bs_rec_off<PH>() + word_off16(r16));
+          if (v.w == 0u) break;
+          uint32_t k[8];
+          load_image(a.hkey, so + bs_img_off<PH>(), k);
+          if (same(k, Rp)) {
+            lpv = __hiloint2double((int)v.y, (int)v.x);
+            ns = (int32_t)v.z;
+            break;
+          }
+        }
+      }
+    }
+    return lpv;
+  }
+  // D_t (planes at layout PH) in state ns, word r (a cursor word parameter): its lookup's loads
+  template <int PH>
+  __device__ void mid_b(const ExpArgs& a, int32_t ns, uint32_t r) {
+    cand = ns == -2 && cvd::bs_bop3<cvd::kTtAndNotOr>(fb1, fw1, cvd::bs_bop3<cvd::kTtAndNotOr>(fb, fw, 0u)) == 0u;
+    slot = ns;
+    hs = hsn | (word_off16(r) >> 4 << kWordShift);
+    if (ns >= 0) {
+      prefetch_row(a, ns, r);
+    } else if (cand) {
+      const uint32_t so = slot_off(hsn);
+      load_image(a.hkey, so + bs_img_off<PH>(), pkey);
+      const uint4 v = ld_off<uint4>(a.hkey, so + bs_rec_off<PH>() + word_off16(r));
+      pc = v.w;
+      pnx = (int32_t)v.z;
+      plp = __hiloint2double((int)v.y, (int)v.x);
+    }
+  }
+  // the lookups' loads are waited for after the ACS that does not need them (every plane of
+  // the new vector: one plane alone lets the scheduler leave the other word's ACS for later) and,
+  // CVD_K1S_DEEP=2, after D_{t+1}'s hash (x2, x3: its results)
+  template <class T>
+  __device__ static void after(T& x, const uint32_t (&N)[2][4], uint32_t x2, uint32_t x3) {
+    asm volatile("" : "+v"(x) : "v"(N[0][0]), "v"(N[0][1]), "v"(N[0][2]), "v"(N[0][3]), "v"(N[1][0]), "v"(N[1][1]),
+                 "v"(N[1][2]), "v"(N[1][3]), "v"(x2), "v"(x3));
+  }
+  __device__ void fence_all(const uint32_t (&N)[2][4], uint32_t x2 = 0u, uint32_t x3 = 0u) {
+    after(slot, N, x2, x3); after(pnx, N, x2, x3); after(plp, N, x2, x3); after(pc, N, x2, x3);
+    after(fw, N, x2, x3); after(fw1, N, x2, x3);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) after(pkey[w], N, x2, x3);
+  }
+  // CVD_K1S_DEEP=2: D_{t+1}'s hash, pattern and pre-filter test before the wait (no loads), its
+  // filter word requested after mid_b (whose test reads D_t's)
+  struct Prep {
+    uint32_t hs, fb, fb1, fo;
+  };
+  template <int PH>
+  __device__ Prep prep(const ExpArgs& a, const uint32_t (&N)[2][4]) const {
+    uint32_t ph, pl;
+    cvd::bs_digest_hash<PH>(N, ph, pl);
+    Prep h;
+    h.hs = ph & a.hmask;
+    const uint2 pp = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(filter_patterns_lds()) +
+                                                     (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 3)));
+    h.fb = pp.x;
+    h.fb1 = pp.y;
+    bool pos = true;
+#if CVD_K1S_PF
+    const uint32_t pfw = reinterpret_cast<const uint32_t*>(dyn_lds())[__builtin_amdgcn_ubfe(
+        pl, 32 - cvd::kBsPfLog2Bits + 5, cvd::kBsPfLog2Bits - 5)];
+    pos = __builtin_amdgcn_ubfe(pfw, pl >> (32 - cvd::kBsPfLog2Bits), 1u) != 0u;
+    if (!pos) {   // (hash_ahead's form: a pattern that filter word 0 cannot match)
+      h.fb = ~0u;
+      h.fb1 = ~0u;
+    }
+#endif
+    h.fo = pos ? (pl & a.fmask4) : 0u;
+    return h;
+  }
+  __device__ void issue(const ExpArgs& a, const Prep& h) {
+    hsn = h.hs;
+    fb = h.fb;
+    fb1 = h.fb1;
+    const uint32_t fo = slot < 0 ? h.fo : 0u;
+#if CVD_K1B_LDSF
+    const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + fo);
+#else
+    const uint2 f = ld_off<uint2>(a.filt, fo);
+#endif
+    fw = f.x;
+    fw1 = f.y;
+  }
+};
+
+template <bool kDeep>
+struct CursorOf {
+  using type = BsCursor;
+};
+template <>
+struct CursorOf<true> {
+  using type = BsDeep;
+};
+
 // H1 waves in walk mode (k1b_walk's schedule; the planes' layout phase is the wave's)
 template <uint64_t XM>
 __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64_t vmask, const double* s_lt) {
@@ -681,20 +829,53 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
     load_chunk(wi >> 2);
     uint32_t cw = pick(wi), nw = pick(wi + 1);
     uint32_t sh = 0u;
-    BsCursor cur;
-    cur.start(a, word_param(cw & 3u), word_param((cw >> 2) & 3u));
+    // (the deep pipeline: the unchunked lockstep loop; chunk units keep the one-step cursor)
+    constexpr bool kDeep = CVD_K1S_DEEP != 0 && !kCk;
+    typename CursorOf<kDeep>::type cur;
+    uint32_t Rp[2][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};   // (deep) D_{t-1}
+    if constexpr (kDeep) {
+      // "D_{-1}" is a known row whose record adds 0.0 (lp = 0.0 + 0.0 + term_0: the same bits)
+      // and names D_0 = 0's row as its successor
+      cur.slot = 0; cur.pnx = a.slot0; cur.plp = 0.0; cur.pc = 1u; cur.cand = false;
+      cur.hs = 0u; cur.hsn = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u; cur.half = 0u;
+    } else {
+      cur.start(a, word_param(cw & 3u), word_param((cw >> 2) & 3u));
+    }
     if (CVD_K1S_ABL & 1) cur.h2wave = hmask == 0u;
     auto step = [&](auto phc, uint32_t rr, uint32_t rn, uint32_t rnn) {
       constexpr int PH = decltype(phc)::value;
       uint32_t Nn[2][4], c;
-      bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
-      lp += cur.template resolve<PH>(a, R, rr, lpu);   // Pd_plotter.py:115, T = P̂1
-      lr += s_lt[c];                                   // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
+      if constexpr (kDeep) {
+        bs_acs<PH, kUni>(R, rr, Nn, c);
+        int32_t ns;
+        if constexpr (CVD_K1S_DEEP == 2) {
+          const typename BsDeep::Prep h = cur.template prep<(PH + 1) % 6>(a, Nn);
+          cur.fence_all(Nn, h.fo, h.fb1);
+          lp += cur.template resolve_a<(PH + 5) % 6>(a, Rp, lpu, ns);   // Pd_plotter.py:115, T = P̂1 (step t - 1)
+          lr += s_lt[c];                                                // Pd_plotter.py:115, T = T_ref(1/2)
+          cur.template mid_b<PH>(a, ns, rr);
+          cur.issue(a, h);
+        } else {
+          cur.fence_all(Nn);
+          lp += cur.template resolve_a<(PH + 5) % 6>(a, Rp, lpu, ns);   // Pd_plotter.py:115, T = P̂1 (step t - 1)
+          lr += s_lt[c];                                                // Pd_plotter.py:115, T = T_ref(1/2)
+          cur.template mid_b<PH>(a, ns, rr);
+          cur.template hash_ahead<(PH + 1) % 6>(a, Nn);
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) Rp[r][i] = R[r][i];
+      } else {
+        bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
+        lp += cur.template resolve<PH>(a, R, rr, lpu);   // Pd_plotter.py:115, T = P̂1
+        lr += s_lt[c];                                   // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
+      }
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
         for (int i = 0; i < 4; ++i) R[r][i] = Nn[r][i];
-      cur.next(a, rn, rnn);
+      if constexpr (!kDeep) cur.next(a, rn, rnn);
     };
     int64_t t = t_begin;
     int grp = 0, dec = 0;
@@ -733,7 +914,8 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
       }
       if (a.early && ++grp == kBsEarlyGroups) {
         grp = 0;
-        if (!dec) dec = early_decide(lp, lr, N - (t + 6), a.lt_min, a.lp_min);
+        // (deep: lp still lacks step t + 5's P̂1 term, so one more remaining increment)
+        if (!dec) dec = early_decide(lp, lr, N - (t + 6) + (kDeep ? 1 : 0), a.lt_min, a.lp_min);
         if (__ballot(dec == 0) == 0) {   // every lane decided: the wave is done
           t = N;
           break;
@@ -741,6 +923,7 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
       }
     }
     // last 1-5 steps
+    const int ntail = (int)(t_end - t);   // (0 after an early exit)
     if (t < t_end) {
       if (ck && t == t_sum) {   // (a last chunk of fewer than six steps)
         ck_store(a, qwave, ck_j, 0u, R);
@@ -754,6 +937,17 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
       if (t + 2 < t_end) step(IntC<2>{}, wk(win, w5, IntC<4>{}), wk(win, w5, IntC<6>{}), w3(win, w5, IntC<8>{}));
       if (t + 3 < t_end) step(IntC<3>{}, wk(win, w5, IntC<6>{}), wk(win, w5, IntC<8>{}), w3(win, w5, IntC<10>{}));
       if (t + 4 < t_end) step(IntC<4>{}, wk(win, w5, IntC<8>{}), wk(win, w5, IntC<10>{}), w3(win, w5, IntC<12>{}));
+    }
+    if constexpr (kDeep) {   // the drain: the last step's lookup (Rp in that step's layout phase)
+      int32_t ns;
+      switch (ntail > 0 ? ntail - 1 : 5) {
+        case 0: lp += cur.template resolve_a<0>(a, Rp, lpu, ns); break;
+        case 1: lp += cur.template resolve_a<1>(a, Rp, lpu, ns); break;
+        case 2: lp += cur.template resolve_a<2>(a, Rp, lpu, ns); break;
+        case 3: lp += cur.template resolve_a<3>(a, Rp, lpu, ns); break;
+        case 4: lp += cur.template resolve_a<4>(a, Rp, lpu, ns); break;
+        default: lp += cur.template resolve_a<5>(a, Rp, lpu, ns); break;
+      }
     }
     if (ck) {   // the chunk's record: D at its end (phase 0 unless it is the last) and its sums
       ck_store(a, qwave, ck_j, 8u, R);

@@ -1971,7 +1971,10 @@ static ExpArgs exp_args(const cvd_model& M, int which, const uint32_t* d_r, int6
     const int e = env_i("CVD_K1S_MIX", -1);
     a.mix = e >= 0 ? (e != 0) : (M.kind == 1 && M.learn_len_eff > 0 && 2 * M.n_rows < M.learn_len_eff);
   }
-  a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;   // two-step walk records
+  // two-step walk records (CVD_WALK_NOT2=1: one 16-B dense record per step instead, a 1.9-MB table
+  // at p = 0.01 against 15 MB; L2 hit rate 0.85 against 0.83, and p = 0.01 1,708-1,730 against
+  // 1,502-1,503 ms per launch, H1 waves alone 1,208 against 1,018: profiles/r06r, r06s)
+  a.t2 = (!M.h_t2.empty() && !std::getenv("CVD_WALK_NOT2")) ? M.d_t2 : nullptr;
   // the k1s walk with the LDS filter reads the compact 8-B records, their log P̂1 values from a
   // table the block copies into LDS after the filter (rtc_t2c, upload_model)
   a.t2c = 0; a.nvtab = 0; a.vtab_off = 0u; a.vtab = nullptr;
