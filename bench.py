@@ -665,25 +665,24 @@ def main():
                 valu["wave_cycles_split"] = {k: cpl.get(c, 0.0) / wc for k, c in (
                     ("issuing", "SQ_ACTIVE_INST_ANY"), ("waiting_on_memory_or_barrier", "SQ_WAIT_ANY"),
                     ("issue_stalled", "SQ_WAIT_INST_ANY"))}
-    # What bounds the m = 6 detector (k1s): dependent row-lookup latency, not HBM bandwidth and
-    # not VALU issue.  The ablations it rests on: removing 5% of the step's
-    # modelled VALU issue cycles (CVD_BS_VFAST) gained <= 1% at p >= 0.05 (profiles/r05aq);
-    # four machine-scheduler strategies land within 0.1% (profiles/r05ae), so instruction order
-    # does not matter; skipping only the H2 waves' L2 filter reads (timing only) shortens p = 0.2
-    # by 9% (profiles/r05w); with the H1 waves' candidate lines cold (profiles/r06_lookup_study.py:
-    # 90-94% of H1 wave-steps at p = 0.05 / 0.1 hold a lane that re-enters a row from a directory
-    # line, 9% / 4% of those rows among the 16k hottest) the waves wait on memory 46-50% of their
-    # cycles at 4 waves per SIMD (SQ_WAIT_ANY, roofline.valu.wave_cycles_split).
-    latency_bound = (not parity and not lds_diag and info.get("kind") == 1 and info.get("explicit_kernel") == 5)
+    # What bounds the m = 6 detector (k1s): VALU issue -- not HBM bandwidth, not lookup bytes and
+    # not lookup latency.  The ablations it rests on (same-box A/Bs): extra VALU per
+    # step (CVD_K1S_PADV, timing only) lengthens p = 0.05 by +3.4 / +6.5 / +15% for 8 / 16 / 32
+    # independent v_bitop3 -- each added instruction costs ~2.3 SIMD-cycles, its full issue cost --
+    # and p = 0.2 by about half that (profiles/r06w); doubling every lookup load's latency budget
+    # (the two-step lookup pipeline, CVD_K1S_DEEP) changes nothing (profiles/r06u); a third fewer
+    # lookup bytes changes nothing (three-line slots, profiles/r06j); the VALU issues one wave64
+    # instruction per 3.65 SIMD-cycles at p = 0.05 (profiles/r06v) against measured issue costs of
+    # 2.4-4.6 cycles per instruction form (profiles/r05an).
+    valu_bound = (not parity and not lds_diag and info.get("kind") == 1 and info.get("explicit_kernel") == 5)
     bound_basis = None
-    if latency_bound:
-        bound_basis = ("dependent row lookups (the L2 filter word of every lookup, cold directory lines of re-entries) "
-                       "at 4 waves per SIMD, together with VALU issue (counted VALU 0.47-0.50 of the 2-cycle peak): not "
-                       "HBM (0.009 of peak) and not lookup bytes (three-line slots: FETCH -18-25%, time +1%, "
-                       "profiles/r06j); -5% modelled VALU issue -> <= 1% at p >= 0.05 (profiles/r05aq); scheduler "
-                       "strategies within 0.1% (profiles/r05ae); less time for the filter word -1.7% (profiles/r06o); "
-                       "H1/H2 waves mixed per SIMD -4.4% at p = 0.05 (profiles/r06k); H2 filter reads skipped (timing "
-                       "only) p = 0.2 -9% (profiles/r05w); waves wait on memory 46-53% of their cycles (SQ_WAIT_ANY)")
+    if valu_bound:
+        bound_basis = ("VALU issue at p >= 0.05 (partly at p = 0.2): +8/+16/+32 independent VALU per step (timing only) "
+                       "-> p = 0.05 +3.4/+6.5/+15%, p = 0.2 +1.6/+3.6/+9%, ~2.3 SIMD-cycles per added v_bitop3 at "
+                       "p = 0.05 = its issue cost (profiles/r06w); one VALU instruction per 3.65 SIMD-cycles against "
+                       "2.4-4.6-cycle issue costs per form (profiles/r06v, r05an); not lookup latency (twice the "
+                       "latency budget for every lookup load: +-0.5%, profiles/r06u); not lookup bytes (three-line "
+                       "slots: FETCH -18-25%, time +1%, profiles/r06j); not HBM (0.009 of peak)")
     elif lds_diag:
         bound_basis = "LDS array busy (roofline.lds, profiles/pmc_lds_<config>.json)"
     c = counts.cpu().numpy()
@@ -725,7 +724,7 @@ def main():
                    "learn_len": info["learn_len_eff"], "model_rows_p0": info["n_rows"],
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "distributed": dist_rec,
-        "roofline": {"bound": "lds" if lds_diag else ("latency" if latency_bound else "hbm"), "achieved": achieved,
+        "roofline": {"bound": "lds" if lds_diag else ("valu" if valu_bound else "hbm"), "achieved": achieved,
                      "bound_basis": bound_basis,
                      "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -913,7 +912,7 @@ def run_c4(a, pkg, world, rank, local, dist):
                    "learn_len": a.learn_len, "early_decision": False,
                    "parallelism": f"dp{world} (trial sharding, one RCCL all_reduce of counts)"},
         "per_N": per_N,
-        "roofline": {"bound": "latency", "achieved": sum(per_N[str(N)]["roofline"]["algorithmic_bytes"] for N in Ns)
+        "roofline": {"bound": "valu", "achieved": sum(per_N[str(N)]["roofline"]["algorithmic_bytes"] for N in Ns)
                      / elapsed / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": sum(per_N[str(N)]["roofline"]["algorithmic_bytes"] for N in Ns) / elapsed / 1e9 / HBM_PEAK_GBS,
                      "traffic": None,

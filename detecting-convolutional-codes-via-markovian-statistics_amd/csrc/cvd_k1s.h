@@ -72,6 +72,11 @@ constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
 #ifndef CVD_K1S_MIDPOS
 #define CVD_K1S_MIDPOS 0
 #endif
+// timing ablation (results unchanged): CVD_K1S_PADV extra VALU instructions per lockstep step,
+// independent of the step's own -- the launch's sensitivity to VALU issue
+#ifndef CVD_K1S_PADV
+#define CVD_K1S_PADV 0
+#endif
 // chunked launches (-DCVD_K1S_CK=0 compiles them out, for A/Bs of the unchunked
 // loop's code: the host then must not chunk, CVD_CHUNK=0)
 #ifndef CVD_K1S_CK
@@ -868,6 +873,17 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
           for (int i = 0; i < 4; ++i) Rp[r][i] = R[r][i];
       } else {
         bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
+#if CVD_K1S_PADV
+        {   // (timing ablation, sums unchanged: CVD_K1S_PADV independent v_bitop3 per step, two chains)
+          uint32_t x = Nn[0][0], y = Nn[1][0];
+#pragma unroll
+          for (int i = 0; i < CVD_K1S_PADV; ++i) {
+            if (i & 1) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(y) : "v"(Nn[1][1]), "v"(Nn[0][2]));
+            else asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x) : "v"(Nn[0][1]), "v"(Nn[1][2]));
+          }
+          asm volatile("" ::"v"(x), "v"(y));
+        }
+#endif
         lp += cur.template resolve<PH>(a, R, rr, lpu);   // Pd_plotter.py:115, T = P̂1
         lr += s_lt[c];                                   // Pd_plotter.py:115, T = T_ref(1/2) = c / 2^n
       }
