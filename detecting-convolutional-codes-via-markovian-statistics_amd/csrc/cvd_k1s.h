@@ -72,6 +72,10 @@ constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
 #ifndef CVD_K1S_MIDPOS
 #define CVD_K1S_MIDPOS 0
 #endif
+// the directory / filter masks of the per-step lookup as VGPR copies (BsCursor::masks)
+#ifndef CVD_K1S_VMASK
+#define CVD_K1S_VMASK 0
+#endif
 // timing ablation (results unchanged): CVD_K1S_PADV extra VALU instructions per lockstep step,
 // independent of the step's own -- the launch's sensitivity to VALU issue
 #ifndef CVD_K1S_PADV
@@ -153,6 +157,18 @@ struct BsCursor {
   bool h2wave = false;   // (CVD_K1S_ABL timing studies: the wave holds H2 sequences only)
   double plp;
   uint32_t pkey[8];
+  // (CVD_K1S_VMASK: the directory and filter masks as VGPR copies made once per unit, so that
+  // their per-step ANDs take the fast all-vector form instead of an SGPR operand)
+  uint32_t vhmask = 0u, vfmask4 = 0u;
+  __device__ void masks(const ExpArgs& a) {
+    if constexpr (CVD_K1S_VMASK != 0) {
+      vhmask = a.hmask;
+      vfmask4 = a.fmask4;
+      asm volatile("" : "+v"(vhmask), "+v"(vfmask4));
+    }
+  }
+  __device__ uint32_t hmask_v(const ExpArgs& a) const { return CVD_K1S_VMASK != 0 ? vhmask : a.hmask; }
+  __device__ uint32_t fmask4_v(const ExpArgs& a) const { return CVD_K1S_VMASK != 0 ? vfmask4 : a.fmask4; }
   // two-step records (a.t2, lockstep lanes that walk learned rows): half 1 = plp / pnx hold the
   // first step of a record whose second is plp2 / pnx2; half 2 = plp / pnx hold that second
   // step, so the next step needs no load
@@ -186,6 +202,7 @@ struct BsCursor {
     half = 1u;
   }
   __device__ void start(const ExpArgs& a, uint32_t r0, uint32_t r1) {
+    masks(a);
     slot = a.slot0; hs = 0u; hsn = 0u; fb = 0u; fw = 0u; fb1 = 0u; fw1 = 0u; cand = false; pc = 1u; half = 0u;
     plp2 = 0.0; pnx2 = -1;
     if (kK1sT2 && a.t2 && !a.t2c) prefetch_t2(a, slot, r0, r1);
@@ -287,7 +304,7 @@ struct BsCursor {
     {
       uint32_t ph, pl;
       cvd::bs_digest_hash<PH>(N, ph, pl);
-      hsn = ph & a.hmask;
+      hsn = ph & hmask_v(a);
       const uint2 pp = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(filter_patterns_lds()) +
                                                        (ph & (uint32_t)((cvd::kFilterPatterns - 1) << 3)));
       fb = pp.x;
@@ -310,7 +327,7 @@ struct BsCursor {
 #else
       constexpr bool pos = true;
 #endif
-      uint32_t fo = slot < 0 && pos && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & a.fmask4) : 0u;
+      uint32_t fo = slot < 0 && pos && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & fmask4_v(a)) : 0u;
       if (CVD_K1S_TRIM & 2) asm volatile("" : "+v"(fo));   // a plain 32-bit offset: the SGPR-base load form
 #if CVD_K1B_LDSF
       const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + fo);
@@ -576,6 +593,7 @@ __device__ __forceinline__ void k1s_walk(const ExpArgs& a, int64_t qwave, uint64
   BsCursor cur;
   cur.slot = -1; cur.pnx = -1; cur.hs = 0u; cur.hsn = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u;
   cur.cand = false; cur.plp = 0.0; cur.pc = 1u; cur.half = 0u; cur.plp2 = 0.0; cur.pnx2 = -1;
+  cur.masks(a);
   double plp2 = 0.0;
   auto two_steps = [&]() -> bool { return a.t2 != nullptr && pos + 2u <= N; };
   auto walk_prefetch = [&]() {
@@ -843,6 +861,7 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
       // and names D_0 = 0's row as its successor
       cur.slot = 0; cur.pnx = a.slot0; cur.plp = 0.0; cur.pc = 1u; cur.cand = false;
       cur.hs = 0u; cur.hsn = 0u; cur.fb = 0u; cur.fw = 0u; cur.fb1 = 0u; cur.fw1 = 0u; cur.half = 0u;
+      cur.masks(a);
     } else {
       cur.start(a, word_param(cw & 3u), word_param((cw >> 2) & 3u));
     }
