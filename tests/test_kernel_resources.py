@@ -27,6 +27,9 @@ VARIANTS = {
     # three-line directory slots (CVD_BS_SLOT3=1, measured and not the default: profiles/r06j)
     "k1s_pf_slot3": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1S_PF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10",
                      "-DCVD_K1S_SLOT3=1"],
+    # the two-step lookup pipeline (CVD_K1S_DEEP=2, measured and not the default: profiles/r06u)
+    "k1s_pf_deep2": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1S_PF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10",
+                     "-DCVD_K1S_DEEP=2"],
 }
 
 
