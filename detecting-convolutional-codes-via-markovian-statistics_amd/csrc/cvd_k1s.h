@@ -131,14 +131,75 @@ __device__ __forceinline__ uint4* bs_etab_lds() {
   __shared__ uint4 s_et[6 * 4 * 2];
   return s_et;
 }
+// CVD_BS_ETAB2 (cvd_bitslice.h bs_step_core_tab): per (phase, y) e0 of both words (8 B) for the
+// zero test, and 128 B of mu-specific addend planes -- mu = 0 at +0, mu = 1 at +64, each
+// {e0m, a1, p1, a23} of word 0, the same of word 1, {p23 of word 0, of word 1}
+#ifndef CVD_BS_ETAB2
+#define CVD_BS_ETAB2 0
+#endif
+__device__ __forceinline__ uint2* bs_e0_lds() {
+  __shared__ uint2 s_e0[6 * 4];
+  return s_e0;
+}
+__device__ __forceinline__ uint4* bs_mt_lds() {
+  __shared__ uint4 s_mt[6 * 4 * 8];
+  return s_mt;
+}
 template <uint64_t XM>
 __device__ __forceinline__ void fill_bs_etab() {
-  uint4* t = bs_etab_lds();
-  for (int i = threadIdx.x; i < 24; i += blockDim.x) {
-    const cvd::BsE E = cvd::bs_eplanes(XM, i >> 2, (uint32_t)(i & 3));
-    t[2 * i] = make_uint4(E.e0[0], E.e1[0], E.ez[0], 0u);
-    t[2 * i + 1] = make_uint4(E.e0[1], E.e1[1], E.ez[1], 0u);
+  if constexpr (CVD_BS_ETAB2 != 0) {
+    uint2* e = bs_e0_lds();
+    uint4* t = bs_mt_lds();
+    for (int i = threadIdx.x; i < 24; i += blockDim.x) {
+      const cvd::BsE E = cvd::bs_eplanes(XM, i >> 2, (uint32_t)(i & 3));
+      e[i] = make_uint2(E.e0[0], E.e0[1]);
+      for (int m = 0; m < 2; ++m) {
+        const cvd::BsMu T = cvd::bs_mu_planes(E, m == 1);
+        uint4* o = t + 8 * i + 4 * m;
+        o[0] = make_uint4(T.e0m[0], T.a1[0], T.p1[0], T.a23[0]);
+        o[1] = make_uint4(T.e0m[1], T.a1[1], T.p1[1], T.a23[1]);
+        o[2] = make_uint4(T.p23[0], T.p23[1], 0u, 0u);
+        o[3] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  } else {
+    uint4* t = bs_etab_lds();
+    for (int i = threadIdx.x; i < 24; i += blockDim.x) {
+      const cvd::BsE E = cvd::bs_eplanes(XM, i >> 2, (uint32_t)(i & 3));
+      t[2 * i] = make_uint4(E.e0[0], E.e1[0], E.ez[0], 0u);
+      t[2 * i + 1] = make_uint4(E.e0[1], E.e1[1], E.ez[1], 0u);
+    }
   }
+}
+// the ACS of one step from the mu-specific planes (CVD_BS_ETAB2); mid as bs_step_core's
+// e0 of both words at (phase PH, word parameter rr) from the LDS table
+template <int PH>
+__device__ __forceinline__ uint2 bs_e0_at(uint32_t rr) {
+  const char* eb = reinterpret_cast<const char*>(bs_e0_lds()) + PH * 32;
+  return *reinterpret_cast<const uint2*>(eb + (kR16 ? (rr >> 1) : 8u * rr));
+}
+template <int PH, bool kUni, class Mid>
+__device__ __forceinline__ void bs_core_tab(const uint32_t (&R)[2][4], uint32_t rr, uint32_t (&N)[2][4], uint32_t& c,
+                                            Mid mid, const uint2* e0pre = nullptr) {
+  // (CVD_BS_ETAB2=2: the lockstep loop read this step's e0 a step ahead, e0pre)
+  const uint2 E0 = e0pre ? *e0pre : bs_e0_at<PH>(rr);
+  const uint32_t e0[2] = {E0.x, E0.y};
+  uint32_t mu;
+  cvd::bs_step_core_tab<PH, kUni>(
+      R, e0,
+      [&](bool zero_hit) {
+        const char* tb = reinterpret_cast<const char*>(bs_mt_lds()) + PH * 512;
+        const uint32_t o = (kR16 ? (rr << 3) : 128u * rr) + (zero_hit ? 0u : 64u);
+        const uint4 w0 = *reinterpret_cast<const uint4*>(tb + o);
+        const uint4 w1 = *reinterpret_cast<const uint4*>(tb + o + 16u);
+        const uint2 q = *reinterpret_cast<const uint2*>(tb + o + 32u);
+        cvd::BsMu T;
+        T.e0m[0] = w0.x; T.a1[0] = w0.y; T.p1[0] = w0.z; T.a23[0] = w0.w;
+        T.e0m[1] = w1.x; T.a1[1] = w1.y; T.p1[1] = w1.z; T.a23[1] = w1.w;
+        T.p23[0] = q.x; T.p23[1] = q.y;
+        return T;
+      },
+      N, mu, c, mid);
 }
 
 // P̂1 row cursor over the bit-sliced tables (RowCursor's protocol: slot >= 0 known row id,
@@ -355,7 +416,17 @@ struct BsCursor {
 // the filter-positive loads issued between the two words' ACS
 template <int PH, bool kUni>
 __device__ __forceinline__ void bs_step(const ExpArgs& a, BsCursor& cur, const uint32_t (&R)[2][4], uint32_t rr,
-                                        uint32_t (&N)[2][4], uint32_t& c) {
+                                        uint32_t (&N)[2][4], uint32_t& c, const uint2* e0pre = nullptr) {
+  if constexpr (CVD_BS_ETAB2 != 0) {
+    static_assert(CVD_K1S_MIDPOS == 0, "CVD_BS_ETAB2 keeps the candidate test between the two words' ACS");
+    bs_core_tab<PH, kUni>(R, rr, N, c, [&](uint32_t dep) {
+      cur.fence_mid(dep);            // dep: the first word's ACS result
+      cur.template mid<PH>(a, rr);
+    }, e0pre);
+    cur.template hash_ahead<(PH + 1) % 6>(a, N);
+    cur.fence_resolve(N[1][3]);
+    return;
+  }
   const uint4* et = kR16 ? reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(bs_etab_lds()) + PH * 128 +
                                                           cvd::bs_shl<1>(rr))
                         : bs_etab_lds() + (PH * 4 + rr) * 2;
@@ -386,6 +457,10 @@ __device__ __forceinline__ void bs_step(const ExpArgs& a, BsCursor& cur, const u
 // the ACS of one step alone (the deep pipeline's lookups run after it)
 template <int PH, bool kUni>
 __device__ __forceinline__ void bs_acs(const uint32_t (&R)[2][4], uint32_t rr, uint32_t (&N)[2][4], uint32_t& c) {
+  if constexpr (CVD_BS_ETAB2 != 0) {
+    bs_core_tab<PH, kUni>(R, rr, N, c, cvd::BsNoMid());
+    return;
+  }
   const uint4* et = kR16 ? reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(bs_etab_lds()) + PH * 128 +
                                                           cvd::bs_shl<1>(rr))
                         : bs_etab_lds() + (PH * 4 + rr) * 2;
@@ -866,6 +941,10 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
       cur.start(a, word_param(cw & 3u), word_param((cw >> 2) & 3u));
     }
     if (CVD_K1S_ABL & 1) cur.h2wave = hmask == 0u;
+    // (CVD_BS_ETAB2=2: each step reads the next step's e0 from LDS, so the zero test does not
+    // wait for it)
+    uint2 e0c = make_uint2(0u, 0u);
+    if constexpr (CVD_BS_ETAB2 == 2 && !kDeep) e0c = bs_e0_at<0>(word_param(cw & 3u));
     auto step = [&](auto phc, uint32_t rr, uint32_t rn, uint32_t rnn) {
       constexpr int PH = decltype(phc)::value;
       uint32_t Nn[2][4], c;
@@ -891,7 +970,13 @@ __device__ __forceinline__ void k1s_wave(const ExpArgs& a, int64_t gw, const dou
 #pragma unroll
           for (int i = 0; i < 4; ++i) Rp[r][i] = R[r][i];
       } else {
-        bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
+        if constexpr (CVD_BS_ETAB2 == 2) {
+          const uint2 e0u = e0c;
+          e0c = bs_e0_at<(PH + 1) % 6>(rn);   // the next step's (its word rn, its phase)
+          bs_step<PH, kUni>(a, cur, R, rr, Nn, c, &e0u);
+        } else {
+          bs_step<PH, kUni>(a, cur, R, rr, Nn, c);
+        }
 #if CVD_K1S_PADV
         {   // (timing ablation, sums unchanged: CVD_K1S_PADV independent v_bitop3 per step, two chains)
           uint32_t x = Nn[0][0], y = Nn[1][0];

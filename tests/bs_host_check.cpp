@@ -5,7 +5,8 @@
 // the reference step's D_t; mu equals the step's minimum; c equals the number of words
 // r' with step(D, r') == D_t (the T_ref count, Pd_plotter.py:89-99); the digest hash of
 // the new planes equals the host key of D_t (bs_digest + bs_key_hash), and bs_canon<f> maps
-// every phase-f digest image to the phase-0 one.  TEST INFRASTRUCTURE ONLY.
+// every phase-f digest image to the phase-0 one; the table form of the step (bs_step_core_tab,
+// CVD_BS_ETAB2) equals the plain one.  TEST INFRASTRUCTURE ONLY.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,6 +64,16 @@ static void run_step(const bs_u32 (&R)[2][4], const BsE& E, bs_u32 (&N)[2][4], b
                      bs_u32& hpl) {
   bs_step_core<PH, kUni>(R, E.e0, E.e1, E.ez, N, mu, c);
   bs_digest_hash<(PH + 1) % 6>(N, hph, hpl);
+  // the table form (CVD_BS_ETAB2) must give the same planes, mu and count
+  bs_u32 N2[2][4], mu2, c2;
+  bs_step_core_tab<PH, kUni>(R, E.e0, [&](bool zero_hit) { return bs_mu_planes(E, !zero_hit); }, N2, mu2, c2);
+  bool same = mu2 == mu && c2 == c;
+  for (int r = 0; r < 2; ++r)
+    for (int i = 0; i < 4; ++i) same = same && N2[r][i] == N[r][i];
+  if (!same) {
+    std::printf("FAIL table step differs at phase %d\n", PH);
+    std::exit(1);
+  }
 }
 
 template <bool kUni>
