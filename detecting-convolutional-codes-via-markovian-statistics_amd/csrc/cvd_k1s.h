@@ -72,6 +72,13 @@ constexpr bool kK1sT2 = CVD_K1S_T2 != 0;
 #ifndef CVD_K1S_MIDPOS
 #define CVD_K1S_MIDPOS 0
 #endif
+// the cursor's per-step selects as sign / bit masks and v_bitop3 (BsCursor::resolve, hash_ahead;
+// default on): static loop cost 3,168 -> 3,069 cycles per six steps, the six-p sweep
+// 1,383,795-1,384,920 -> 1,389,060-1,390,175 trials/s on one box (profiles/r06ad, three rounds),
+// sums identical (119 GPU parity tests)
+#ifndef CVD_K1S_AMASK
+#define CVD_K1S_AMASK 1
+#endif
 // the directory / filter masks of the per-step lookup as VGPR copies (BsCursor::masks)
 #ifndef CVD_K1S_VMASK
 #define CVD_K1S_VMASK 0
@@ -323,7 +330,36 @@ struct BsCursor {
     double lpv = lpu;
     int32_t ns = pfpos ? -2 : -1;   // D_t's lookup pending, or settled by the pre-filter
     const bool known = slot >= 0;
-    if (known) {
+    if constexpr (CVD_K1S_AMASK != 0 && (CVD_K1S_TRIM & 1) == 0) {
+      // (the known row's record or the pending state by a sign mask and three v_bitop3 -- not a
+      // compare and three selects on it; a candidate implies slot == -2, so it needs no `known`)
+      const uint32_t m = (uint32_t)(slot >> 31);   // ~0: D_{t-1}'s row is not known
+      ns = (int32_t)cvd::bs_bop3<cvd::kTtSel>(m, (uint32_t)-2, (uint32_t)pnx);
+      lpv = __hiloint2double((int)cvd::bs_bop3<cvd::kTtSel>(m, (uint32_t)__double2hiint(lpu), (uint32_t)__double2hiint(plp)),
+                             (int)cvd::bs_bop3<cvd::kTtSel>(m, (uint32_t)__double2loint(lpu), (uint32_t)__double2loint(plp)));
+    }
+    if (CVD_K1S_AMASK != 0 && (CVD_K1S_TRIM & 1) == 0) {
+      if (cand) {
+        if (same(pkey, R)) {
+          lpv = plp; ns = pnx;
+        } else if (pc != 0u) {
+          uint32_t sl = hs;
+          for (int pr = 1; pr <= a.max_probe; ++pr) {
+            sl = (sl + 1u) & a.hmask;
+            const uint32_t so = slot_off(sl);
+            const uint4 v = ld_off<uint4>(a.hkey, so + bs_rec_off<PH>() + word_off16(r));
+            if (v.w == 0u) break;
+            uint32_t k[8];
+            load_image(a.hkey, so + bs_img_off<PH>(), k);
+            if (same(k, R)) {
+              lpv = __hiloint2double((int)v.y, (int)v.x);
+              ns = (int32_t)v.z;
+              break;
+            }
+          }
+        }
+      }
+    } else if (known) {
       lpv = plp; ns = pnx;
     } else if (cand) {
       if (same(pkey, R)) {
@@ -382,17 +418,29 @@ struct BsCursor {
           pl, 32 - cvd::kBsPfLog2Bits + 5, cvd::kBsPfLog2Bits - 5)];
       // (bit (pl >> (32 - kBsPfLog2Bits)) mod 32 of the word: the extract takes the offset's
       // low five bits)
-      const bool pos = __builtin_amdgcn_ubfe(pfw, pl >> (32 - cvd::kBsPfLog2Bits), 1u) != 0u;
-      if (CVD_K1S_TRIM & 1) {
-        pfpos = pos;
-      } else if (!pos) {
-        fb = ~0u;
-        fb1 = ~0u;
+      const uint32_t pbit = __builtin_amdgcn_ubfe(pfw, pl >> (32 - cvd::kBsPfLog2Bits), 1u);
+      const bool pos = pbit != 0u;
+      uint32_t fo;
+      if constexpr (CVD_K1S_AMASK != 0 && (CVD_K1S_TRIM & 1) == 0 && (CVD_K1S_ABL & 1) == 0) {
+        // (masks instead of compares and selects: pm = ~0 where the bit is set, sm = ~0 where
+        // D_{t-1}'s row is not known; a clear bit makes the pattern all-ones, as below)
+        const uint32_t pm = 0u - pbit, sm = (uint32_t)(slot >> 31);
+        fb = cvd::bs_bop3<0xF3>(fb, pm, 0u);    // fb | ~pm
+        fb1 = cvd::bs_bop3<0xF3>(fb1, pm, 0u);
+        fo = cvd::bs_bop3<0x80>(pl, pm, sm) & fmask4_v(a);
+      } else {
+        if (CVD_K1S_TRIM & 1) {
+          pfpos = pos;
+        } else if (!pos) {
+          fb = ~0u;
+          fb1 = ~0u;
+        }
+        fo = slot < 0 && pos && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & fmask4_v(a)) : 0u;
       }
 #else
       constexpr bool pos = true;
-#endif
       uint32_t fo = slot < 0 && pos && !((CVD_K1S_ABL & 1) && h2wave) ? (pl & fmask4_v(a)) : 0u;
+#endif
       if (CVD_K1S_TRIM & 2) asm volatile("" : "+v"(fo));   // a plain 32-bit offset: the SGPR-base load form
 #if CVD_K1B_LDSF
       const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(dyn_lds()) + fo);
