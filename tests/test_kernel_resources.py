@@ -27,6 +27,10 @@ VARIANTS = {
     # three-line directory slots (CVD_BS_SLOT3=1, measured and not the default: profiles/r06j)
     "k1s_pf_slot3": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1S_PF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10",
                      "-DCVD_K1S_SLOT3=1"],
+    # the select-form ACS and compare-form cursor (CVD_BS_ETAB2=0, CVD_K1S_AMASK=0: the forms before
+    # round 6's VALU cuts, kept for A/Bs)
+    "k1s_pf_select_forms": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1S_PF=1", "-DCVD_K1B_BLOCK=1024",
+                            "-DCVD_FILTER_PAT_BITS=10", "-DCVD_BS_ETAB2=0", "-DCVD_K1S_AMASK=0"],
     # the two-step lookup pipeline (CVD_K1S_DEEP=2, measured and not the default: profiles/r06u)
     "k1s_pf_deep2": ["-DCVD_K1B_BITSLICE=1", "-DCVD_K1S_PF=1", "-DCVD_K1B_BLOCK=1024", "-DCVD_FILTER_PAT_BITS=10",
                      "-DCVD_K1S_DEEP=2"],
