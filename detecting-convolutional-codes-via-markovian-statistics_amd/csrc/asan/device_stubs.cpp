@@ -14,6 +14,7 @@ int cvd::explicit_kernel_of(const cvd_model& M) { return M.k1b_ok ? CVD_KERNEL_B
 bool cvd::mc_fused_preferred(const cvd_model&) { return false; }
 bool cvd::walk_preferred(const cvd_model&, bool) { return false; }
 bool cvd::ldsf_preferred(const cvd_model&) { return false; }
+bool cvd::ldsf_wanted(const cvd_model&) { return false; }
 int64_t cvd::multi_variant(const cvd_model&) { return 0; }
 int64_t cvd::persist_seqs(const cvd_model&) { return 0; }
 int64_t cvd::persist_grid(const cvd_model&, int64_t) { return 0; }

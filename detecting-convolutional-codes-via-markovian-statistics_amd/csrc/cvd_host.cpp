@@ -516,7 +516,7 @@ void build_hash(cvd_model& Mo) {
   // cvd_kernels.hip): up to 4 keys per two-word block, ~0.06% false positives, against an
   // L2 read per H2 step.
   const bool bsp = bitslice_preferred(Mo);
-  const bool ldsf = walk_preferred(Mo) && Mo.n_rows <= ldsf_max_rows(bsp) && !std::getenv("CVD_NO_LDSF");
+  const bool ldsf = ldsf_wanted(Mo) && Mo.n_rows <= ldsf_max_rows(bsp) && !std::getenv("CVD_NO_LDSF");
   int fscale = 0, fmax_log2 = ldsf ? ldsf_log2(bsp) : 19;
   if (const char* e = std::getenv("CVD_FILTER_SCALE")) fscale = std::max(-3, std::min(3, std::atoi(e)));
   if (const char* e = std::getenv("CVD_FILTER_MAX_LOG2")) fmax_log2 = std::max(8, std::min(28, std::atoi(e)));

@@ -165,6 +165,10 @@ int ldsf_log2(bool bs);
 bool bs_pf_preferred(const cvd_model& M, bool ldsf);
 int64_t ldsf_max_rows(bool bs);
 bool ldsf_preferred(const cvd_model& M);
+// the model is a candidate for the whole Bloom filter in LDS: it walks, or (CVD_LDSF_LOCKSTEP=1)
+// any model small enough, whose lockstep lanes then read the LDS filter instead of the
+// pre-filter and the L2 filter
+bool ldsf_wanted(const cvd_model& M);
 int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
                     uint32_t tag, uint64_t thr, int64_t N, int64_t trial_begin, int64_t T, double* d_sums,
                     int64_t* d_counts, void* stream, bool early);

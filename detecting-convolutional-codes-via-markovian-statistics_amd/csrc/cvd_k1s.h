@@ -138,39 +138,43 @@ __device__ __forceinline__ uint4* bs_etab_lds() {
   __shared__ uint4 s_et[6 * 4 * 2];
   return s_et;
 }
-// CVD_BS_ETAB2 (default 1; cvd_bitslice.h bs_step_core_tab): per (phase, y) e0 of both words (8 B)
-// for the zero test, and 128 B of mu-specific addend planes -- mu = 0 at +0, mu = 1 at +64, each
-// {e0m, a1, p1, a23} of word 0, the same of word 1, {p23 of word 0, of word 1} -- read at the
-// offset mu selects instead of selecting the planes with the mu mask: 8 VALU fewer per step.
+// CVD_BS_ETAB2 (default 1; cvd_bitslice.h bs_step_core_tab): per (phase, y) e0 of both words for
+// the zero test, and the mu-specific addend planes -- {e0m, a1, p1, a23} of word 0, the same of
+// word 1, {p23 of word 0, of word 1} -- read at the offset mu selects instead of selecting the
+// planes with the mu mask: 8 VALU fewer per step.
 // Same sums (119 GPU parity tests); the six-p sweep 1,375,820-1,377,109 -> 1,397,206-1,399,600
 // trials/s on one box (profiles/r06ab, three rounds); =2 (the next step's e0 read a step ahead)
 // 1,396,238-1,399,600, the same; =0 the select form
 #ifndef CVD_BS_ETAB2
 #define CVD_BS_ETAB2 1
 #endif
-__device__ __forceinline__ uint2* bs_e0_lds() {
-  __shared__ uint2 s_e0[6 * 4];
+// (16-B strides per word y, so that the word parameter 16 y is the byte offset itself and the
+// phase and mu parts are the reads' immediate offsets and one add: e0 at [phase][y] in 16-B
+// slots; the mu planes in three sub-tables of [phase][mu][y] 16-B slots each)
+constexpr uint32_t kBsMtSub = 6 * 2 * 4 * 16;   // bytes per mu sub-table
+__device__ __forceinline__ uint4* bs_e0_lds() {
+  __shared__ uint4 s_e0[6 * 4];
   return s_e0;
 }
 __device__ __forceinline__ uint4* bs_mt_lds() {
-  __shared__ uint4 s_mt[6 * 4 * 8];
+  __shared__ uint4 s_mt[3 * 6 * 2 * 4];
   return s_mt;
 }
 template <uint64_t XM>
 __device__ __forceinline__ void fill_bs_etab() {
   if constexpr (CVD_BS_ETAB2 != 0) {
-    uint2* e = bs_e0_lds();
+    uint4* e = bs_e0_lds();
     uint4* t = bs_mt_lds();
     for (int i = threadIdx.x; i < 24; i += blockDim.x) {
-      const cvd::BsE E = cvd::bs_eplanes(XM, i >> 2, (uint32_t)(i & 3));
-      e[i] = make_uint2(E.e0[0], E.e0[1]);
+      const int ph = i >> 2, y = i & 3;
+      const cvd::BsE E = cvd::bs_eplanes(XM, ph, (uint32_t)y);
+      e[i] = make_uint4(E.e0[0], E.e0[1], 0u, 0u);
       for (int m = 0; m < 2; ++m) {
         const cvd::BsMu T = cvd::bs_mu_planes(E, m == 1);
-        uint4* o = t + 8 * i + 4 * m;
-        o[0] = make_uint4(T.e0m[0], T.a1[0], T.p1[0], T.a23[0]);
-        o[1] = make_uint4(T.e0m[1], T.a1[1], T.p1[1], T.a23[1]);
-        o[2] = make_uint4(T.p23[0], T.p23[1], 0u, 0u);
-        o[3] = make_uint4(0u, 0u, 0u, 0u);
+        const int k = (ph * 2 + m) * 4 + y;   // 16-B slot in each sub-table
+        t[k] = make_uint4(T.e0m[0], T.a1[0], T.p1[0], T.a23[0]);
+        t[k + kBsMtSub / 16] = make_uint4(T.e0m[1], T.a1[1], T.p1[1], T.a23[1]);
+        t[k + 2 * (kBsMtSub / 16)] = make_uint4(T.p23[0], T.p23[1], 0u, 0u);
       }
     }
   } else {
@@ -186,8 +190,8 @@ __device__ __forceinline__ void fill_bs_etab() {
 // e0 of both words at (phase PH, word parameter rr) from the LDS table
 template <int PH>
 __device__ __forceinline__ uint2 bs_e0_at(uint32_t rr) {
-  const char* eb = reinterpret_cast<const char*>(bs_e0_lds()) + PH * 32;
-  return *reinterpret_cast<const uint2*>(eb + (kR16 ? (rr >> 1) : 8u * rr));
+  const char* eb = reinterpret_cast<const char*>(bs_e0_lds()) + PH * 64;
+  return *reinterpret_cast<const uint2*>(eb + word_off16(rr));
 }
 template <int PH, bool kUni, class Mid>
 __device__ __forceinline__ void bs_core_tab(const uint32_t (&R)[2][4], uint32_t rr, uint32_t (&N)[2][4], uint32_t& c,
@@ -199,11 +203,11 @@ __device__ __forceinline__ void bs_core_tab(const uint32_t (&R)[2][4], uint32_t 
   cvd::bs_step_core_tab<PH, kUni>(
       R, e0,
       [&](bool zero_hit) {
-        const char* tb = reinterpret_cast<const char*>(bs_mt_lds()) + PH * 512;
-        const uint32_t o = (kR16 ? (rr << 3) : 128u * rr) + (zero_hit ? 0u : 64u);
+        const char* tb = reinterpret_cast<const char*>(bs_mt_lds()) + PH * 128;
+        const uint32_t o = word_off16(rr) + (zero_hit ? 0u : 64u);
         const uint4 w0 = *reinterpret_cast<const uint4*>(tb + o);
-        const uint4 w1 = *reinterpret_cast<const uint4*>(tb + o + 16u);
-        const uint2 q = *reinterpret_cast<const uint2*>(tb + o + 32u);
+        const uint4 w1 = *reinterpret_cast<const uint4*>(tb + o + kBsMtSub);
+        const uint2 q = *reinterpret_cast<const uint2*>(tb + o + 2u * kBsMtSub);
         cvd::BsMu T;
         T.e0m[0] = w0.x; T.a1[0] = w0.y; T.p1[0] = w0.z; T.a23[0] = w0.w;
         T.e0m[1] = w1.x; T.a1[1] = w1.y; T.p1[1] = w1.z; T.a23[1] = w1.w;

@@ -1894,21 +1894,30 @@ int cvd::explicit_kernel_of(const cvd_model& M) {
 // filter of 128 KiB 543.8 / 643.4 (blocks of 16 waves wait for their slowest wave: 1,024
 // threads with the global filter 570.9 / 668.7, 512 threads 541.6 / 625.7).  CVD_NO_LDSF=1
 // keeps the filter in global memory.
+// The bit-sliced kernel's lockstep lanes read the whole filter from LDS too (CVD_LDSF_LOCKSTEP,
+// default 1 for it): no pre-filter and no L2 filter word per lookup.  p = 0.01 (29,626 rows):
+// 1,300-1,309 ms per launch against 1,395-1,397 with the pre-filter and L2 filter and 1,472-1,474
+// walking (profiles/r06ai, same sums)
+bool cvd::ldsf_wanted(const cvd_model& M) {
+  const bool bs = M.rtc_fn ? M.rtc_bs : bitslice_preferred(M);
+  return walk_preferred(M) || (env_i("CVD_LDSF_LOCKSTEP", bs ? 1 : 0) == 1);
+}
 bool cvd::ldsf_preferred(const cvd_model& M) {
-  return !std::getenv("CVD_NO_LDSF") && walk_preferred(M) && M.n_rows <= ldsf_max_rows(M.bs) &&
+  return !std::getenv("CVD_NO_LDSF") && ldsf_wanted(M) && M.n_rows <= ldsf_max_rows(M.bs) &&
          M.fcap <= ((int64_t)1 << ldsf_log2(M.bs)) && M.h_filt_lds.size() == (size_t)M.fcap;
 }
 
 bool cvd::walk_preferred(const cvd_model& M, bool early) {
   const int e = env_i("CVD_WALK", -1);
   if (e >= 0) return e != 0;
-  // the bit-sliced kernel's lockstep steps are cheaper, so it walks only below 1/20: p = 0.02
-  // (70,134 rows / 10^6) runs 1,584 ms lockstep against 1,703 walking, p = 0.01 (29,626) 1,433
-  // walking against 1,534 (profiles/r05r_p*/)
+  // the bit-sliced kernel does not walk by default: its lockstep steps are cheaper (round 5:
+  // p = 0.02 1,584 ms lockstep against 1,703 walking, profiles/r05r_p*/), and since round 6's
+  // table-form ACS and lockstep LDS filter p = 0.01 too (1,300-1,309 ms against 1,472-1,474
+  // walking, profiles/r06ai); the butterfly kernel walks below rows / learn_len = 1/10
   // (keyed on the kernel that runs once the JIT has decided -- a model whose bit-sliced build
   // failed runs the butterfly kernel, ADVICE r05 -- else on the tables' prediction)
-  const int64_t ratio = (M.rtc_fn ? M.rtc_bs : bitslice_preferred(M)) ? 20 : 10;
-  return !early && M.kind == 1 && M.learn_len_eff > 0 && ratio * M.n_rows < M.learn_len_eff;
+  if (M.rtc_fn ? M.rtc_bs : bitslice_preferred(M)) return false;
+  return !early && M.kind == 1 && M.learn_len_eff > 0 && 10 * M.n_rows < M.learn_len_eff;
 }
 
 // the persistent launch's blocks (CVD_K1S_PERSIST=0: never; CVD_K1S_PERSIST_BLOCKS=b: at most b,

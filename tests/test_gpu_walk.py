@@ -116,16 +116,18 @@ def test_walk_early_decision_counts(pkg, monkeypatch, p):
 
 
 def test_walk_flag_follows_row_share(pkg, monkeypatch):
-    """cvd_model_info.walk: on where the model's rows / learn_len < 1/20 (H1 stays in rows;
-    the bit-sliced kernel's threshold), off elsewhere and for dense models; CVD_WALK forces it."""
+    """cvd_model_info.walk: the bit-sliced kernel runs lockstep at every p by default (round 6:
+    p = 0.01 lockstep with the LDS filter 1,300 against 1,472 ms walking), with the whole filter
+    in LDS where the rows fit (p = 0.01); off for dense models; CVD_WALK forces it."""
     cc, det = _m6(pkg)
     monkeypatch.delenv("CVD_WALK", raising=False)
+    monkeypatch.delenv("CVD_LDSF_LOCKSTEP", raising=False)
     lo = det.model(0.01, 1_000_000, 200, 1.0, SEED).info()
     hi = det.model(0.1, 1_000_000, 200, 1.0, SEED).info()
-    assert 20 * lo["n_rows"] < lo["learn_len_eff"] and lo["walk"] == 1
-    assert 20 * hi["n_rows"] >= hi["learn_len_eff"] and hi["walk"] == 0
-    mid = det.model(0.02, 1_000_000, 200, 1.0, SEED).info()   # 70,134 rows: lockstep
-    assert 20 * mid["n_rows"] >= mid["learn_len_eff"] and mid["walk"] == 0
+    assert lo["walk"] == 0 and lo["lds_filter"] == 1 and lo["n_rows"] <= 32768
+    assert hi["walk"] == 0 and hi["lds_filter"] == 0
+    mid = det.model(0.02, 1_000_000, 200, 1.0, SEED).info()   # 70,134 rows: lockstep, filter in L2
+    assert mid["walk"] == 0 and mid["lds_filter"] == 0
     monkeypatch.setenv("CVD_WALK", "1")
     assert det.model(0.1, 1_000_000, 200, 1.0, SEED).info()["walk"] == 1
     m2 = pkg.CONFIG_CODES["m2"]
@@ -135,27 +137,29 @@ def test_walk_flag_follows_row_share(pkg, monkeypatch):
 
 
 def test_lds_filter_equals_global_filter(pkg, monkeypatch):
-    """cvd_model_info.lds_filter: walking models of <= 32,768 rows keep a 64 KiB Bloom filter
-    in LDS (512-thread blocks); the sums equal the global-filter kernel's (CVD_NO_LDSF=1,
-    256-thread blocks, the filter sized >= 32 bits per row) and the lockstep run's."""
+    """cvd_model_info.lds_filter: models of <= 32,768 rows keep their whole Bloom filter in
+    LDS (the lockstep default, and walk mode); the sums equal the global-filter kernel's
+    (CVD_NO_LDSF=1: the pre-filter and the L2 filter) and the walking run's."""
     cc, det = _m6(pkg)
     p, N, t0, t1 = 0.01, 3001, 17, 17 + 700
-    monkeypatch.delenv("CVD_WALK", raising=False)
-    monkeypatch.delenv("CVD_NO_LDSF", raising=False)
+    for v in ("CVD_WALK", "CVD_NO_LDSF", "CVD_LDSF_LOCKSTEP"):
+        monkeypatch.delenv(v, raising=False)
     # fresh models (Detector.model keeps one per key): the filter is sized at build, the
     # kernel variant chosen at upload
     lds = pkg.Model(det.dec, p, 300_000, 200, 1.0, SEED).upload(0)
-    assert lds.info()["walk"] == 1 and lds.info()["lds_filter"] == 1
+    assert lds.info()["walk"] == 0 and lds.info()["lds_filter"] == 1
     got, gc = _sums(det, lds, cc, N, p, t0, t1)
     monkeypatch.setenv("CVD_NO_LDSF", "1")
     glob = pkg.Model(det.dec, p, 300_000, 200, 1.0, SEED).upload(0)
     assert glob.info()["lds_filter"] == 0
     ref, rc = _sums(det, glob, cc, N, p, t0, t1)
     monkeypatch.delenv("CVD_NO_LDSF")
-    monkeypatch.setenv("CVD_WALK", "0")
-    lock, lc = _sums(det, lds, cc, N, p, t0, t1)
-    assert np.array_equal(got, ref) and np.array_equal(lock, ref)
-    assert gc == rc == lc
+    monkeypatch.setenv("CVD_WALK", "1")
+    walk = pkg.Model(det.dec, p, 300_000, 200, 1.0, SEED).upload(0)
+    assert walk.info()["walk"] == 1 and walk.info()["lds_filter"] == 1
+    wk, wc = _sums(det, walk, cc, N, p, t0, t1)
+    assert np.array_equal(got, ref) and np.array_equal(wk, ref)
+    assert gc == rc == wc
     assert pkg.Model(det.dec, 0.1, 300_000, 200, 1.0, SEED).upload(0).info()["lds_filter"] == 0
 
 
@@ -183,7 +187,9 @@ def test_lds_filter_model_under_jit_fallbacks(pkg, monkeypatch, how):
     # info.walk reports what runs: walk mode needs the specialised kernel
     if how == "hiprtc":
         # (the bit-sliced form k1s if the hipRTC compiler takes it, else the butterfly kernel)
-        assert inf["explicit_kernel"] in (4, 5) and inf["lds_filter"] == 1 and inf["walk"] == 1
+        # (walk mode only where the butterfly kernel is what runs: the bit-sliced one stays lockstep)
+        assert inf["explicit_kernel"] in (4, 5) and inf["lds_filter"] == 1
+        assert inf["walk"] == (1 if inf["explicit_kernel"] == 4 else 0)
     else:
         assert inf["explicit_kernel"] == 3 and inf["lds_filter"] == 0 and inf["walk"] == 0
     got, gc = _sums(det, alt, cc, N, p, t0, t1)
@@ -198,6 +204,7 @@ def test_walk_guard_flag_is_reported(pkg, monkeypatch):
     cc = pkg.CONFIG_CODES["m6"]
     det = pkg.Detector(1, 2, 6, cc["gen1"], device=0)
     monkeypatch.setenv("CVD_JIT_DEFINES", "-DCVD_WALK_GUARD=0")
+    monkeypatch.setenv("CVD_WALK", "1")
     model = pkg.Model(det.dec, 0.01, 300_000, 200, 1.0, 7).upload(0)
     assert model.info()["walk"] == 1
     with pytest.raises(pkg.CvdError, match="scheduler guard"):

@@ -158,25 +158,29 @@ def test_directory_sizing(pkg, monkeypatch):
 
 def test_walk_and_lds_filter_flags(pkg, monkeypatch):
     """cvd_model_info.walk / lds_filter before upload (cvd_kernels.hip walk_preferred,
-    ldsf_preferred): a model whose rows / learn_len < 1/20 walks (the bit-sliced kernel's
-    threshold; 1/10 for the nibble kernel), and one of <= 32,768 rows
-    also keeps its Bloom filter in LDS; CVD_NO_LDSF=1 (read at build) turns that off and
-    CVD_WALK=0 both."""
+    ldsf_wanted, ldsf_preferred): the bit-sliced kernel does not walk by default (round 6:
+    lockstep with the LDS filter is faster at p = 0.01), and a model of <= 32,768 rows keeps its
+    whole Bloom filter in LDS (CVD_LDSF_LOCKSTEP, default on for the bit-sliced kernel);
+    CVD_NO_LDSF=1 (read at build) turns the LDS filter off, CVD_LDSF_LOCKSTEP=0 too unless the
+    model walks, and CVD_WALK=1 forces walk mode (with the LDS filter)."""
     taps = [[[1, 0, 1, 1, 0, 1, 1]], [[1, 1, 1, 1, 0, 0, 1]]]
     code = pkg.Code(taps, 6, 1, 2)
-    for v in ("CVD_WALK", "CVD_NO_LDSF"):
+    for v in ("CVD_WALK", "CVD_NO_LDSF", "CVD_LDSF_LOCKSTEP"):
         monkeypatch.delenv(v, raising=False)
     inf = pkg.Model(code, 0.01, 300_000, 200, 1.0, 7).info()
     assert 20 * inf["n_rows"] < inf["learn_len_eff"] and inf["n_rows"] <= 32768
-    assert inf["walk"] == 1 and inf["lds_filter"] == 1
-    hi = pkg.Model(code, 0.1, 20_000, 200, 1.0, 7).info()
-    assert hi["walk"] == 0 and hi["lds_filter"] == 0
+    assert inf["walk"] == 0 and inf["lds_filter"] == 1
+    hi = pkg.Model(code, 0.2, 60_000, 200, 1.0, 7).info()   # > 32,768 rows: the filter stays in L2
+    assert hi["n_rows"] > 32768 and hi["walk"] == 0 and hi["lds_filter"] == 0
     monkeypatch.setenv("CVD_NO_LDSF", "1")
     assert pkg.Model(code, 0.01, 300_000, 200, 1.0, 7).info()["lds_filter"] == 0
     monkeypatch.delenv("CVD_NO_LDSF")
-    monkeypatch.setenv("CVD_WALK", "0")
+    monkeypatch.setenv("CVD_LDSF_LOCKSTEP", "0")
     off = pkg.Model(code, 0.01, 200_000, 200, 1.0, 7).info()
     assert off["walk"] == 0 and off["lds_filter"] == 0
+    monkeypatch.setenv("CVD_WALK", "1")
+    on = pkg.Model(code, 0.01, 200_000, 200, 1.0, 7).info()
+    assert on["walk"] == 1 and on["lds_filter"] == 1
 
 
 @pytest.mark.parametrize("name,kernel", [("m6_133_171", 3), ("m3_demo", 3), ("m2_75", 2), ("r23_m4", 1)])
