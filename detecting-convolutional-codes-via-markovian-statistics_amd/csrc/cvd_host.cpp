@@ -844,9 +844,14 @@ int cvd::ldsf_log2(bool bs) {
   const char* e = std::getenv("CVD_LDSF_LOG2");
   return e && *e ? std::max(13, std::min(15, std::atoi(e))) : (bs ? 15 : kLdsFilterLog2);
 }
+// (the bit-sliced kernel's lockstep lanes gain from the 128-KiB LDS filter up to p = 0.02's
+// 70,134 rows: 1,442-1,443 ms per launch against 1,497-1,499 with the pre-filter and L2 filter,
+// profiles/r06ak; at p = 0.05's 315,953 rows it is saturated, 4,770-4,789 against 1,860,
+// profiles/r06al: so up to 3 x 32,768 rows)
 int64_t cvd::ldsf_max_rows(bool bs) {
   const char* e = std::getenv("CVD_LDSF_MAX_ROWS");
-  return e && *e ? (int64_t)std::atoll(e) : kLdsFilterMaxRows << std::max(0, ldsf_log2(bs) - (bs ? 15 : kLdsFilterLog2));
+  return e && *e ? (int64_t)std::atoll(e)
+                 : (bs ? 3 : 1) * (kLdsFilterMaxRows << std::max(0, ldsf_log2(bs) - (bs ? 15 : kLdsFilterLog2)));
 }
 
 bool cvd::bs_pf_preferred(const cvd_model& M, bool ldsf) {

@@ -118,7 +118,7 @@ def test_walk_early_decision_counts(pkg, monkeypatch, p):
 def test_walk_flag_follows_row_share(pkg, monkeypatch):
     """cvd_model_info.walk: the bit-sliced kernel runs lockstep at every p by default (round 6:
     p = 0.01 lockstep with the LDS filter 1,300 against 1,472 ms walking), with the whole filter
-    in LDS where the rows fit (p = 0.01); off for dense models; CVD_WALK forces it."""
+    in LDS where the rows fit (p = 0.01, 0.02); off for dense models; CVD_WALK forces it."""
     cc, det = _m6(pkg)
     monkeypatch.delenv("CVD_WALK", raising=False)
     monkeypatch.delenv("CVD_LDSF_LOCKSTEP", raising=False)
@@ -126,8 +126,8 @@ def test_walk_flag_follows_row_share(pkg, monkeypatch):
     hi = det.model(0.1, 1_000_000, 200, 1.0, SEED).info()
     assert lo["walk"] == 0 and lo["lds_filter"] == 1 and lo["n_rows"] <= 32768
     assert hi["walk"] == 0 and hi["lds_filter"] == 0
-    mid = det.model(0.02, 1_000_000, 200, 1.0, SEED).info()   # 70,134 rows: lockstep, filter in L2
-    assert mid["walk"] == 0 and mid["lds_filter"] == 0
+    mid = det.model(0.02, 1_000_000, 200, 1.0, SEED).info()   # 70,134 rows: the LDS filter too
+    assert mid["walk"] == 0 and mid["lds_filter"] == 1
     monkeypatch.setenv("CVD_WALK", "1")
     assert det.model(0.1, 1_000_000, 200, 1.0, SEED).info()["walk"] == 1
     m2 = pkg.CONFIG_CODES["m2"]
@@ -137,7 +137,7 @@ def test_walk_flag_follows_row_share(pkg, monkeypatch):
 
 
 def test_lds_filter_equals_global_filter(pkg, monkeypatch):
-    """cvd_model_info.lds_filter: models of <= 32,768 rows keep their whole Bloom filter in
+    """cvd_model_info.lds_filter: models of <= 98,304 rows keep their whole Bloom filter in
     LDS (the lockstep default, and walk mode); the sums equal the global-filter kernel's
     (CVD_NO_LDSF=1: the pre-filter and the L2 filter) and the walking run's."""
     cc, det = _m6(pkg)

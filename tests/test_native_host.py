@@ -159,7 +159,7 @@ def test_directory_sizing(pkg, monkeypatch):
 def test_walk_and_lds_filter_flags(pkg, monkeypatch):
     """cvd_model_info.walk / lds_filter before upload (cvd_kernels.hip walk_preferred,
     ldsf_wanted, ldsf_preferred): the bit-sliced kernel does not walk by default (round 6:
-    lockstep with the LDS filter is faster at p = 0.01), and a model of <= 32,768 rows keeps its
+    lockstep with the LDS filter is faster at p = 0.01), and a model of <= 98,304 rows keeps its
     whole Bloom filter in LDS (CVD_LDSF_LOCKSTEP, default on for the bit-sliced kernel);
     CVD_NO_LDSF=1 (read at build) turns the LDS filter off, CVD_LDSF_LOCKSTEP=0 too unless the
     model walks, and CVD_WALK=1 forces walk mode (with the LDS filter)."""
@@ -170,8 +170,8 @@ def test_walk_and_lds_filter_flags(pkg, monkeypatch):
     inf = pkg.Model(code, 0.01, 300_000, 200, 1.0, 7).info()
     assert 20 * inf["n_rows"] < inf["learn_len_eff"] and inf["n_rows"] <= 32768
     assert inf["walk"] == 0 and inf["lds_filter"] == 1
-    hi = pkg.Model(code, 0.2, 60_000, 200, 1.0, 7).info()   # > 32,768 rows: the filter stays in L2
-    assert hi["n_rows"] > 32768 and hi["walk"] == 0 and hi["lds_filter"] == 0
+    hi = pkg.Model(code, 0.2, 120_000, 200, 1.0, 7).info()   # > 98,304 rows: the filter stays in L2
+    assert hi["n_rows"] > 98304 and hi["walk"] == 0 and hi["lds_filter"] == 0
     monkeypatch.setenv("CVD_NO_LDSF", "1")
     assert pkg.Model(code, 0.01, 300_000, 200, 1.0, 7).info()["lds_filter"] == 0
     monkeypatch.delenv("CVD_NO_LDSF")
