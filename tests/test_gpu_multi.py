@@ -106,6 +106,8 @@ def test_multi_runs_persistent_batches_alone(pkg, monkeypatch):
     ps = [0.02, 0.05, 0.1, 0.2]
     T = [1500, 300, 2100, 700]
     N = 2001
+    # (one kernel variant for all four: p = 0.02's rows would otherwise take the LDS filter)
+    monkeypatch.setenv("CVD_LDSF_LOCKSTEP", "0")
     cc, det, models, bufs = _setup(pkg, ps, N, T)
     nseq = [2 * t for t in T]
 
