@@ -152,8 +152,8 @@ int launch_detect_table(const cvd_model& M, const uint32_t* d_r, int64_t N, int6
 bool mc_fused_preferred(const cvd_model& M);
 // the specialised butterfly kernel runs the model's H1 waves in walk mode (k1b_walk)
 bool walk_preferred(const cvd_model& M, bool early = false);
-// LDS-resident Bloom filter of the specialised kernel: walking models of at most
-// kLdsFilterMaxRows rows, whose filter is built with 2^kLdsFilterLog2 words (64 KiB, <= 4
+// LDS-resident Bloom filter of the specialised kernel (ldsf_wanted: walking models, and
+// bit-sliced lockstep models unless CVD_LDSF_LOCKSTEP=0) of at most ldsf_max_rows rows, whose filter is built with 2^kLdsFilterLog2 words (64 KiB, <= 4
 // keys per two-word block, ~0.06% false positives) for 512-thread blocks, two per CU
 constexpr int kLdsFilterLog2 = 14;
 constexpr int64_t kLdsFilterMaxRows = 32768;
@@ -165,8 +165,8 @@ int ldsf_log2(bool bs);
 bool bs_pf_preferred(const cvd_model& M, bool ldsf);
 int64_t ldsf_max_rows(bool bs);
 bool ldsf_preferred(const cvd_model& M);
-// the model is a candidate for the whole Bloom filter in LDS: it walks, or (CVD_LDSF_LOCKSTEP=1)
-// any model small enough, whose lockstep lanes then read the LDS filter instead of the
+// the model is a candidate for the whole Bloom filter in LDS: it walks, or (CVD_LDSF_LOCKSTEP,
+// default 1 for bit-sliced models, 0 otherwise) any model small enough, whose lockstep lanes then read the LDS filter instead of the
 // pre-filter and the L2 filter
 bool ldsf_wanted(const cvd_model& M);
 int launch_mc_fused(const cvd_model& M, const CodeDesc& e1, const CodeDesc& e2, uint32_t k0, uint32_t k1,
