@@ -125,10 +125,29 @@ CVD_HD bs_u32 bs_perm(bs_u32 hi, bs_u32 lo, bs_u32 sel) {
 #ifndef CVD_BS_VFAST
 #define CVD_BS_VFAST 15
 #endif
+// CVD_BS_KLDS (timing A/B, default 0): the six flip / canonicalisation masks come from a
+// block-shared table (filled with the kernel's other LDS tables) instead of a v_mov per use
+// group: an LDS read the compiler may keep in a VGPR across the step loop
+#ifndef CVD_BS_KLDS
+#define CVD_BS_KLDS 0
+#endif
+constexpr int bs_kmask_index(bs_u32 C) {
+  return C == 0xAAAAAAAAu ? 0 : C == 0xCCCCCCCCu ? 1 : C == 0xF0F0F0F0u ? 2
+       : C == 0x55555555u ? 3 : C == 0x33333333u ? 4 : C == 0x0F0F0F0Fu ? 5 : -1;
+}
+constexpr bs_u32 kBsKmasks[6] = {0xAAAAAAAAu, 0xCCCCCCCCu, 0xF0F0F0F0u, 0x55555555u, 0x33333333u, 0x0F0F0F0Fu};
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__) || defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ bs_u32* bs_kmask_lds() {
+  __shared__ bs_u32 s_km[8];
+  return s_km;
+}
+#endif
 template <bs_u32 C>
 CVD_HD bs_u32 bs_vconst() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr ((CVD_BS_VFAST & 1) != 0) {
+  if constexpr (CVD_BS_KLDS != 0 && bs_kmask_index(C) >= 0) {
+    return bs_kmask_lds()[bs_kmask_index(C)];
+  } else if constexpr ((CVD_BS_VFAST & 1) != 0) {
     bs_u32 c;
     asm volatile("v_mov_b32 %0, %1" : "=v"(c) : "i"(C));
     return c;

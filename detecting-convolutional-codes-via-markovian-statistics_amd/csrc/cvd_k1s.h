@@ -162,6 +162,9 @@ __device__ __forceinline__ uint4* bs_mt_lds() {
 }
 template <uint64_t XM>
 __device__ __forceinline__ void fill_bs_etab() {
+  if constexpr (CVD_BS_KLDS != 0) {
+    if (threadIdx.x < 6) cvd::bs_kmask_lds()[threadIdx.x] = cvd::kBsKmasks[threadIdx.x];
+  }
   if constexpr (CVD_BS_ETAB2 != 0) {
     uint4* e = bs_e0_lds();
     uint4* t = bs_mt_lds();
